@@ -1,0 +1,296 @@
+#!/usr/bin/env python3
+"""bench.py -- CISTA-LSTC inference throughput on MI355X (BASELINE.json config c2).
+
+Metric: reconstructed frames/s at 180x240, 5-bin voxels, depth 5, base_channels 64.
+One STEP = one len_sequence (15) recurrent pass over B sequences per GPU: states carried
+frame to frame, prev_image = previous output (reference test_e2v.py:105-117 semantics),
+starting from prev_states=None / zero image.  Inputs (synthetic voxels, built on the GPU from
+15 000 random events each, reference utils/event_process.py recipe) are resident in HBM before
+the timed region.  value = frames of ALL ranks / max-over-ranks wall time of K steps.
+
+Multi-GPU: one process per GPU (torchrun), sequences sharded across ranks with no data-path
+collective (inference replicas: "scaling": "weak"); only the timing max and a barrier use RCCL.
+
+Also reported on the same JSON line:
+  roofline      -- the dominant kernel's achieved algorithmic TFLOP/s (HIP events on the stream
+                   it is launched on) against the fp16-MFMA dense peak divided by the 3 passes
+                   of the split-fp16 scheme;
+  cpu_baseline  -- rank 0 only: the numpy CPU restatement (oracle/, "kind": "port") timed on this
+                   host over a bounded sample, and the PSNR / max relative error of the GPU frames
+                   against it on the same inputs ("PSNR vs ref" of the metric).
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import math
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+MACS_PER_FRAME_C64 = 22_793_011_200          # 180x240, C=64, depth 5, bins 5
+PEAK_F16_MFMA_TFLOPS = 2500.0                # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
+SPLIT_PASSES = 3
+
+
+def parse():
+    p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=3)
+    p.add_argument("--warmup", type=int, default=1)
+    p.add_argument("--batch", type=int, default=64, help="sequences per GPU")
+    p.add_argument("--len-seq", type=int, default=15)
+    p.add_argument("--height", type=int, default=180)
+    p.add_argument("--width", type=int, default=240)
+    p.add_argument("--num-events", type=int, default=15000)
+    p.add_argument("--cpu-frames", type=int, default=6,
+                   help="frames of the bounded CPU-baseline sample (one sequence, B=1)")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--layer-reps", type=int, default=10)
+    return p.parse_args()
+
+
+# ------------------------------------------------------------------ synthetic inputs (GPU)
+def synth_voxels(torch, n_frames, n_seq, nb, H, W, n_events, seed, device):
+    """(n_frames, n_seq, nb, H, W) fp32 voxels: per voxel n_events events with sorted
+    t ~ U(0, 0.05), x, y uniform, p in {-1, +1}; temporal-bilinear binning and the nonzero
+    mean/std normalisation with hot-pixel filter (reference utils/event_process.py:15-63,
+    132-154) written with torch ops on the device."""
+    g = torch.Generator(device=device).manual_seed(seed)
+    V = n_frames * n_seq
+    t = torch.sort(torch.rand(V, n_events, generator=g, device=device, dtype=torch.float64) * 0.05, 1)[0]
+    x = torch.randint(0, W, (V, n_events), generator=g, device=device)
+    y = torch.randint(0, H, (V, n_events), generator=g, device=device)
+    p = torch.randint(0, 2, (V, n_events), generator=g, device=device).to(torch.float64) * 2 - 1
+    dT = (t[:, -1:] - t[:, :1]).clamp_min(1e-12)
+    ts = (nb - 1) * (t - t[:, :1]) / dT
+    ti = ts.floor().long()
+    dt = ts - ti
+    base = torch.arange(V, device=device)[:, None] * (nb * H * W) + y * W + x
+    vox = torch.zeros(V * nb * H * W, device=device, dtype=torch.float64)
+    ok = ti < nb
+    vox.index_add_(0, (base + ti * H * W)[ok], (p * (1 - dt))[ok])
+    ok = (ti + 1) < nb
+    vox.index_add_(0, (base + (ti + 1) * H * W)[ok], (p * dt)[ok])
+    vox = vox.view(V, nb * H * W).float()
+    vox[vox.abs() > 25.0 / nb] = 0
+    nz = (vox != 0).float()
+    n = nz.sum(1, keepdim=True).clamp_min(1)
+    mean = vox.sum(1, keepdim=True) / n
+    std = torch.sqrt((vox * vox).sum(1, keepdim=True) / n - mean * mean)
+    vox = nz * (vox - mean) / (std + 1e-8)
+    return vox.view(n_frames, n_seq, nb, H, W).contiguous()
+
+
+def he_init_(torch, model, seed):
+    """Random-init weights of the architecture, He-scaled so that the recurrence is not
+    trivially saturated (the default init gives ~0.5 everywhere)."""
+    g = torch.Generator().manual_seed(seed)
+    with torch.no_grad():
+        for name, prm in model.named_parameters():
+            if name.endswith("Lambda"):
+                prm.fill_(0.05)
+            elif prm.dim() == 4:
+                fan_in = prm.shape[1] * 9
+                prm.copy_(torch.randn(prm.shape, generator=g) / math.sqrt(fan_in))
+            else:
+                prm.copy_(torch.rand(prm.shape, generator=g) * 0.2 - 0.1)
+
+
+def run_sequence(torch, model, vox_seq, B, H, W, device):
+    prev = torch.zeros(B, 1, H, W, device=device)
+    states = None
+    for f in range(vox_seq.shape[0]):
+        prev, states = model(vox_seq[f], prev, states)
+    return prev, states
+
+
+def time_layers(torch, model, lib_mod, vox, B, H, W, device, reps):
+    """Average duration of every kernel of the frame schedule, measured with HIP events on the
+    stream the library launches on (torch's current stream, passed explicitly)."""
+    L = lib_mod.lib()
+    C = model.base_channels
+    h, w = H // 2, W // 2
+    with torch.no_grad():
+        rec0, st0 = model(vox[0], torch.zeros(B, 1, H, W, device=device), None)
+        cl = torch.channels_last
+        outs = dict(rec=torch.empty(B, 1, H, W, device=device),
+                    c_lstc=torch.empty(B, 2 * C, h, w, device=device, memory_format=cl),
+                    z=torch.empty(B, 2 * C, h, w, device=device, memory_format=cl),
+                    h=torch.empty(B, C, h, w, device=device, memory_format=cl),
+                    c=torch.empty(B, C, h, w, device=device, memory_format=cl))
+        ws = model.workspace(B, H, W, device)
+        packed = model.packed_params()
+        ev = vox[1].contiguous()
+        io = lib_mod.CistaFrameIO(ev.data_ptr(), rec0.data_ptr(), st0[0].data_ptr(),
+                                  st0[1].data_ptr(), st0[2][0].data_ptr(), st0[2][1].data_ptr(),
+                                  outs["rec"].data_ptr(), outs["c_lstc"].data_ptr(),
+                                  outs["z"].data_ptr(), outs["h"].data_ptr(), outs["c"].data_ptr())
+        cfg = model._cfg()
+        stream = torch.cuda.current_stream(device)
+        lib_mod.check(L.cista_forward(ctypes.byref(cfg), packed.data_ptr(), B, H, W, ctypes.byref(io),
+                                      ws.data_ptr(), ws.numel(), stream.cuda_stream), "forward")
+        res = {}
+        for lid, name in enumerate(lib_mod.LAYERS):
+            for _ in range(2):
+                lib_mod.check(L.cista_launch_layer(ctypes.byref(cfg), packed.data_ptr(), lid, B, H, W,
+                                                   ctypes.byref(io), ws.data_ptr(), ws.numel(),
+                                                   stream.cuda_stream), name)
+            e0 = torch.cuda.Event(enable_timing=True)
+            e1 = torch.cuda.Event(enable_timing=True)
+            e0.record(stream)
+            for _ in range(reps):
+                L.cista_launch_layer(ctypes.byref(cfg), packed.data_ptr(), lid, B, H, W,
+                                     ctypes.byref(io), ws.data_ptr(), ws.numel(), stream.cuda_stream)
+            e1.record(stream)
+            e1.synchronize()
+            ms = e0.elapsed_time(e1) / reps
+            macs = L.cista_layer_macs(ctypes.byref(cfg), lid, B, H, W)
+            per_frame = model.depth if name in ("ista_D", "ista_P") else 1
+            res[name] = dict(ms=ms, macs=macs, launches_per_frame=per_frame,
+                             tflops=2 * macs / (ms * 1e-3) / 1e12)
+        torch.cuda.synchronize()
+    return res
+
+
+def psnr(a, b):
+    """utils/evaluate.py:18-28 (PIXEL_MAX = 1, 100 if mse < 1e-10)."""
+    import numpy as np
+    mse = float(np.mean((np.asarray(a, np.float64) - np.asarray(b, np.float64)) ** 2))
+    return 100.0 if mse < 1e-10 else 20 * math.log10(1.0 / math.sqrt(mse))
+
+
+def cpu_baseline(torch, model, vox, H, W, n_frames):
+    """Bounded CPU sample: the numpy restatement (oracle/) on ONE sequence of n_frames frames
+    at full size; returns the timing and the GPU-vs-CPU agreement on that sequence."""
+    import numpy as np
+    from oracle import fixtures as fx
+    from oracle.cista_oracle import CistaLSTCOracle
+    try:
+        from threadpoolctl import threadpool_info
+        cores = max([i.get("num_threads", 1) for i in threadpool_info()] or [1])
+    except Exception:  # pragma: no cover
+        cores = os.cpu_count()
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    oracle = CistaLSTCOracle(fx.collapse_tied(sd, model.depth), model.depth, np.float32)
+    v = vox[:n_frames, :1].cpu().numpy()
+    t0 = time.perf_counter()
+    o_recs, _ = oracle.run_sequence(v)
+    dt = time.perf_counter() - t0
+    with torch.no_grad():
+        prev = torch.zeros(1, 1, H, W, device=vox.device)
+        states = None
+        g_recs = []
+        for f in range(n_frames):
+            prev, states = model(vox[f, :1], prev, states)
+            g_recs.append(prev.cpu().numpy())
+    g_recs = np.stack(g_recs)
+    rel = float(np.abs(g_recs - o_recs).max() / np.abs(o_recs).max())
+    ps = float(np.mean([psnr(g_recs[f], o_recs[f]) for f in range(n_frames)]))
+    return dict(value=n_frames / dt, unit="frames/s", cores=int(cores), kind="port",
+                sample=f"1 sequence x {n_frames} recurrent frames at {H}x{W} (B=1), numpy oracle "
+                       f"(oracle/cista_oracle.py), {dt:.1f} s"), ps, rel
+
+
+def main():
+    args = parse()
+    rank = int(os.environ.get("RANK", 0))
+    world = int(os.environ.get("WORLD_SIZE", 1))
+    local_rank = int(os.environ.get("LOCAL_RANK", 0))
+    import torch
+    import torch.distributed as dist
+    from v2e2v_amd import CistaLSTCNet, _lib
+
+    device = torch.device("cuda", local_rank)
+    torch.cuda.set_device(device)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+    B, L, H, W = args.batch, args.len_seq, args.height, args.width
+
+    model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
+    he_init_(torch, model, seed=7)
+    model = model.to(device).eval()
+    # sequences of this rank: a disjoint shard (seed offset by rank)
+    vox = synth_voxels(torch, L, B, 5, H, W, args.num_events, seed=1000 + rank, device=device)
+    torch.cuda.synchronize()
+
+    with torch.no_grad():
+        for _ in range(args.warmup):
+            run_sequence(torch, model, vox, B, H, W, device)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rec, _ = run_sequence(torch, model, vox, B, H, W, device)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        elapsed = time.perf_counter() - t0
+    finite = bool(torch.isfinite(rec).all())
+    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed = float(t.item())
+    frames = world * B * L * args.steps
+    value = frames / elapsed
+
+    layers = time_layers(torch, model, _lib, vox, B, H, W, device, args.layer_reps)
+    dom_name = max(layers, key=lambda k: layers[k]["ms"] * layers[k]["launches_per_frame"])
+    dom = layers[dom_name]
+    peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
+    roofline = dict(bound="mfma", achieved=round(dom["tflops"], 2), peak=round(peak, 1),
+                    unit="TFLOP/s", frac=round(dom["tflops"] / peak, 4), traffic=None,
+                    kernel=dom_name, launch_ms=round(dom["ms"], 4),
+                    flop_per_launch=2 * dom["macs"],
+                    note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean "
+                         "duration; peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+
+    cpu = None
+    psnr_vs_ref = rel_vs_ref = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu, psnr_vs_ref, rel_vs_ref = cpu_baseline(torch, model, vox, H, W,
+                                                    min(args.cpu_frames, L))
+
+    if rank == 0:
+        frame_ms = sum(v["ms"] * v["launches_per_frame"] for v in layers.values())
+        out = {
+            "metric": "reconstructed frames/sec/GPU at 180x240 5-bin depth=5; PSNR vs ref",
+            "value": round(value, 2),
+            "unit": "frames/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 3),
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (GPU-generated 15000-event voxels; He-scaled random-init weights)",
+            "config": {"workload": f"CISTA-LSTC inference {H}x{W} 5-bin depth=5 C=64, "
+                                   f"len_sequence={L}, {B} sequences/GPU",
+                       "batch_per_gpu": B, "len_sequence": L, "height": H, "width": W,
+                       "num_events": args.num_events, "parallelism": f"replicas x{world}",
+                       "precision": "split3-f16 MFMA (fp32 accumulate)"},
+            "frames_per_s_per_gpu": round(value / world, 2),
+            "tflops_effective": round(value * 2 * MACS_PER_FRAME_C64 / 1e12, 2),
+            "psnr_vs_ref": None if psnr_vs_ref is None else round(psnr_vs_ref, 2),
+            "max_rel_err_vs_ref": rel_vs_ref,
+            "outputs_finite": finite,
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+            "layers_ms": {k: round(v["ms"], 4) for k, v in layers.items()},
+            "layers_tflops": {k: round(v["tflops"], 1) for k, v in layers.items()},
+            "sum_of_kernels_ms_per_frame_batch": round(frame_ms, 3),
+        }
+        print(json.dumps(out), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

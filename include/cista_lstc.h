@@ -1,0 +1,164 @@
+/*
+ * cista_lstc.h -- C ABI of the MI355X-native CISTA-LSTC event-to-video hot path
+ * (libcista_hip.so, built for gfx950).
+ *
+ * The reference exposes this path only as a Python nn.Module (lsying009/V2E2V has no native
+ * code and no FFI), so each entry point below replaces one reference Python call site; a
+ * ctypes binding (v2e2v_amd/_lib.py) sits between them and the unchanged
+ * `CistaLSTCNet` surface:
+ *
+ *   cista_pack_params      <- nn.Conv2d parameter storage of CistaLSTCNet.__init__
+ *                             (reference e2v/e2v_model.py:6-38); re-run after every
+ *                             load_state_dict / optimizer step (weights -> split-bf16 MFMA tiles)
+ *   cista_forward          <- CistaLSTCNet.forward(events, prev_image, prev_states)
+ *                             (reference e2v/e2v_model.py:41-90)
+ *   cista_stage_input      <- We / Wi / cat / W0                 (e2v_model.py:62-66)
+ *   cista_stage_lstc       <- ConvLSTC.forward                   (e2v/base_layers.py:52-71)
+ *   cista_stage_ista       <- tied IstaBlock loop + softshrink   (e2v_model.py:72-78,
+ *                                                                  base_layers.py:11-12)
+ *   cista_stage_decoder    <- RecurrentConvLayer + ConvLSTM      (base_layers.py:214-225,90-130)
+ *   cista_stage_output     <- UpsampleConvLayer + final_conv + sigmoid
+ *                                                                 (base_layers.py:193-210,
+ *                                                                  e2v_model.py:85-88)
+ *
+ * Conventions (all functions):
+ *   - plain C types only; `stream` is a hipStream_t passed as void* (NULL = legacy default);
+ *   - every tensor argument is a DEVICE pointer to fp32 data;
+ *   - events (B, num_bins, H, W) and frames (B, 1, H, W) are NCHW (== the module surface);
+ *     recurrent states are NHWC ("channels_last"), half resolution h = H/2, w = W/2:
+ *       c_lstc, z : (B, h, w, 2*C)        h, c : (B, h, w, C)
+ *   - a NULL previous-state pointer means "None" in the reference (zeros), per state;
+ *   - outputs never alias inputs (checked: CISTA_ERR_ALIAS); inputs are never written;
+ *   - work is only enqueued on `stream` (no host sync, no allocation) -> graph-capturable;
+ *   - return value: CISTA_OK or an error code; cista_status_string() describes it.  The Python
+ *     shim turns every non-zero status into a RuntimeError, like the reference's torch errors.
+ */
+#ifndef CISTA_LSTC_H
+#define CISTA_LSTC_H
+
+#include <stddef.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CISTA_ABI_VERSION 1
+
+enum {
+    CISTA_OK = 0,
+    CISTA_ERR_INVALID = 1,      /* bad shape / NULL pointer / inconsistent arguments        */
+    CISTA_ERR_UNSUPPORTED = 2,  /* valid in the reference but not built here (e.g. C % 32)  */
+    CISTA_ERR_HIP = 3,          /* a HIP runtime call failed                                */
+    CISTA_ERR_WORKSPACE = 4,    /* workspace smaller than cista_workspace_bytes()           */
+    CISTA_ERR_ALIAS = 5         /* an output buffer overlaps an input buffer                */
+};
+
+/* CistaLSTCNet(image_dim, base_channels, depth, num_bins) -- image_dim is unused by the
+ * reference forward (e2v_model.py:13), so it is not part of the config. */
+typedef struct {
+    int base_channels;   /* C; this build requires C % 32 == 0 (reference default 64) */
+    int depth;           /* ISTA iterations (tied weights), >= 0                        */
+    int num_bins;        /* voxel bins, >= 1                                            */
+} cista_config;
+
+/* The 25 UNIQUE parameter tensors, device fp32, reference layouts
+ * (conv weight [Cout][Cin][3][3], bias [Cout], Lambda [1][2C][1][1]).
+ * Gate orders follow the reference: P0.gates = (in, forget) (base_layers.py:58),
+ * Dg.recurrent_block.Gates = (in, remember, out, cell) (base_layers.py:116). */
+typedef struct {
+    const float *We_w, *We_b;                 /* We.conv2d            [C/2][nb][3][3]   */
+    const float *Wi_w, *Wi_b;                 /* Wi.conv2d            [C/2][1][3][3]    */
+    const float *W0_w, *W0_b;                 /* W0.conv2d            [C][C][3][3], s2  */
+    const float *gates_w, *gates_b;           /* P0.gates             [4C][3C][3][3]    */
+    const float *out_gates_w, *out_gates_b;   /* P0.out_gates         [2C][4C][3][3]    */
+    const float *P0_w, *P0_b;                 /* P0.P0                [2C][C][3][3]     */
+    const float *lambda;                      /* lista_blocks.*.Lambda [1][2C][1][1]    */
+    const float *D_w, *D_b;                   /* lista_blocks.*.D     [C][2C][3][3]     */
+    const float *P_w, *P_b;                   /* lista_blocks.*.P     [2C][C][3][3]     */
+    const float *Dg_w, *Dg_b;                 /* Dg.conv.conv2d       [C][2C][3][3]     */
+    const float *lstm_w, *lstm_b;             /* Dg.recurrent_block.Gates [4C][2C][3][3]*/
+    const float *up_w, *up_b;                 /* upsamp_conv.conv2d   [C][C][3][3]      */
+    const float *final_w, *final_b;           /* final_conv.conv2d    [1][C][3][3]      */
+} cista_params;
+
+typedef struct {
+    const float *events;       /* (B, nb, H, W) NCHW                                 */
+    const float *prev_image;   /* (B, 1, H, W)                                       */
+    const float *c_lstc_prev;  /* prev_states[0]    NHWC (B,h,w,2C) or NULL          */
+    const float *z_prev;       /* prev_states[1]    NHWC (B,h,w,2C) or NULL          */
+    const float *h_prev;       /* prev_states[2][0] NHWC (B,h,w,C)  or NULL          */
+    const float *c_prev;       /* prev_states[2][1] NHWC (B,h,w,C)  (NULL iff h_prev)*/
+    float *rec;                /* out (B, 1, H, W) in (0, 1)                          */
+    float *c_lstc;             /* out states[0] NHWC (B,h,w,2C)                       */
+    float *z;                  /* out states[1] NHWC (B,h,w,2C)                       */
+    float *h;                  /* out states[2][0] NHWC (B,h,w,C)                     */
+    float *c;                  /* out states[2][1] NHWC (B,h,w,C)                     */
+} cista_frame_io;
+
+int         cista_abi_version(void);
+const char *cista_status_string(int status);
+
+/* packed (MFMA-tiled, split-bf16) parameter blob */
+size_t cista_packed_bytes(const cista_config *cfg);
+int    cista_pack_params(const cista_config *cfg, const cista_params *params, void *packed,
+                         void *stream);
+
+/* scratch needed by cista_forward / the stage entries for one (B, H, W) */
+size_t cista_workspace_bytes(const cista_config *cfg, int B, int H, int W);
+
+/* one recurrent frame for B independent sequences */
+int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int W,
+                  const cista_frame_io *io, void *workspace, size_t workspace_bytes,
+                  void *stream);
+
+/* ---- stage entries (the reference module boundaries; used by parity tests) ---- */
+/* x1 (B,h,w,C) NHWC = W0(cat(We(events), Wi(prev_image)))                              */
+int cista_stage_input(const cista_config *cfg, const void *packed, int B, int H, int W,
+                      const float *events, const float *prev_image, float *x1,
+                      void *workspace, size_t workspace_bytes, void *stream);
+/* ConvLSTC: (z_out, c_out) = P0(x1, z_prev, c_prev); z0 scratch inside workspace        */
+int cista_stage_lstc(const cista_config *cfg, const void *packed, int B, int h, int w,
+                     const float *x1, const float *z_prev, const float *c_prev,
+                     float *z_out, float *c_out, void *workspace, size_t workspace_bytes,
+                     void *stream);
+/* z <- S_lambda(z + P(x1 - D(z))) applied `iters` times IN PLACE on z (B,h,w,2C)        */
+int cista_stage_ista(const cista_config *cfg, const void *packed, int B, int h, int w,
+                     const float *x1, float *z, int iters, void *workspace,
+                     size_t workspace_bytes, void *stream);
+/* (h_out, c_out) = ConvLSTM(relu(Dg.conv(z)), (h_prev, c_prev))                          */
+int cista_stage_decoder(const cista_config *cfg, const void *packed, int B, int h, int w,
+                        const float *z, const float *h_prev, const float *c_prev,
+                        float *h_out, float *c_out, void *workspace, size_t workspace_bytes,
+                        void *stream);
+/* rec (B,1,2h,2w) = sigmoid(final_conv(relu(upsamp_conv(h)))); pre_sigmoid may be NULL   */
+int cista_stage_output(const cista_config *cfg, const void *packed, int B, int h, int w,
+                       const float *hstate, float *rec, float *pre_sigmoid, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
+/* ---- measurement hook (bench.py): launch exactly ONE kernel of the frame schedule on the
+ * buffers of a previous cista_forward with the same io/workspace, so its duration can be
+ * timed with events on `stream`.  Not a reference interface.  layer ids: */
+enum {
+    CISTA_LAYER_INPUT = 0,      /* We/Wi (VALU)                     */
+    CISTA_LAYER_W0 = 1,         /* stride-2 conv                    */
+    CISTA_LAYER_P0 = 2,
+    CISTA_LAYER_GATES = 3,      /* ConvLSTC gates + cell update     */
+    CISTA_LAYER_OUT_GATES = 4,
+    CISTA_LAYER_ISTA_D = 5,
+    CISTA_LAYER_ISTA_P = 6,
+    CISTA_LAYER_DG = 7,
+    CISTA_LAYER_LSTM = 8,
+    CISTA_LAYER_UPSAMPLE = 9,
+    CISTA_LAYER_FINAL = 10,
+    CISTA_LAYER_COUNT = 11
+};
+/* multiply-accumulates of one launch of `layer` (per frame x B) -- the algorithmic work */
+double cista_layer_macs(const cista_config *cfg, int layer, int B, int H, int W);
+int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, int B, int H,
+                       int W, const cista_frame_io *io, void *workspace, size_t workspace_bytes,
+                       void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CISTA_LSTC_H */

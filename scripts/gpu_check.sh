@@ -1,0 +1,28 @@
+#!/bin/bash
+# One GPU-box session: parity tests -> smoke -> bench (-> optional rocprof).  Every GPU step has
+# its own time limit; after a crash / fault / timeout nothing else touches the GPU.
+# usage: bash scripts/gpu_check.sh [tests] [smoke] [bench] [prof] [pmc]
+mkdir -p gpurun_out
+ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test failures, not a crash
+for step in "$@"; do
+  case "$step" in
+    tests)
+      timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+      rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log; ok $rc || exit $rc ;;
+    smoke)
+      timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
+      rc=$?; echo "smoke rc=$rc"; tail -2 gpurun_out/smoke.log; [ $rc -eq 0 ] || exit $rc ;;
+    bench)
+      timeout -k 10 600 python bench.py ${BENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/bench.json 2> gpurun_out/bench.err
+      rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc ;;
+    prof)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
+      rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.err; [ $rc -eq 0 ] || exit $rc ;;
+    pmc)
+      for ctr in FETCH_SIZE WRITE_SIZE; do
+        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -d gpurun_out/pmc_$ctr -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --layer-reps 3 > /dev/null 2> gpurun_out/pmc_$ctr.err
+        rc=$?; echo "pmc $ctr rc=$rc"; tail -2 gpurun_out/pmc_$ctr.err; [ $rc -eq 0 ] || exit $rc
+      done ;;
+  esac
+done

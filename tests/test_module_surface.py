@@ -1,0 +1,80 @@
+"""Drop-in boundary checks that need no GPU: the C-ABI library loads and exports every symbol
+include/cista_lstc.h declares; the nn.Module surface (ctor, 45-key state_dict, tied weights,
+checkpoint layout, init RNG stream) matches the reference; and the product path refuses to run
+on CPU instead of falling back to anything."""
+import ctypes
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from tests.conftest import GOLDEN
+from v2e2v_amd import CistaLSTCNet, _lib
+
+
+def test_library_exports_every_header_symbol():
+    L = _lib.lib()
+    names = _lib.header_functions()
+    assert len(names) >= 11
+    for n in names:
+        assert hasattr(L, n), n
+    assert L.cista_abi_version() == 1
+    for s in range(6):
+        assert L.cista_status_string(s)
+
+
+def test_sizes_and_invalid_config():
+    L = _lib.lib()
+    cfg = _lib.CistaConfig(64, 5, 5)
+    assert L.cista_packed_bytes(ctypes.byref(cfg)) > 1404481 * 4 // 2
+    assert L.cista_workspace_bytes(ctypes.byref(cfg), 2, 64, 64) > 0
+    bad = _lib.CistaConfig(0, 5, 5)
+    assert L.cista_packed_bytes(ctypes.byref(bad)) == 0
+    assert L.cista_workspace_bytes(ctypes.byref(cfg), 0, 64, 64) == 0
+    # host-side validation happens before any device work: no GPU needed
+    io = _lib.CistaFrameIO()
+    st = L.cista_forward(ctypes.byref(cfg), None, 1, 64, 64, ctypes.byref(io), None, 0, None)
+    assert st == 1
+    odd = _lib.CistaConfig(48, 5, 5)   # base_channels % 32 != 0 -> unsupported, not wrong
+    assert L.cista_forward(ctypes.byref(odd), ctypes.c_void_p(1), 1, 64, 64,
+                           ctypes.byref(io), None, 0, None) == 2
+
+
+def test_state_dict_layout_and_default_init_match_reference():
+    ck = torch.load(os.path.join(GOLDEN, "f1_default.pth.tar"), weights_only=True)
+    assert set(ck) == {"epoch", "state_dict"}
+    torch.manual_seed(0)
+    np.random.seed(0)
+    m = CistaLSTCNet([64, 64], base_channels=64, depth=5, num_bins=5)
+    sd = m.state_dict()
+    assert list(sd) == list(ck["state_dict"])             # 45 keys, reference order
+    assert len(sd) == 45
+    for k, v in ck["state_dict"].items():
+        assert sd[k].shape == v.shape
+        assert torch.equal(sd[k], v), k                    # same RNG draws, same order
+    assert sum(p.numel() for p in m.parameters()) == 1404481
+    m.load_state_dict(ck["state_dict"], strict=True)
+
+
+def test_tied_ista_last_copy_wins():
+    m = CistaLSTCNet([32, 32], base_channels=32, depth=3, num_bins=5)
+    sd = m.state_dict()
+    sd = {k: v.clone() for k, v in sd.items()}
+    sd["lista_blocks.0.Lambda"].fill_(1.0)
+    sd["lista_blocks.2.Lambda"].fill_(7.0)
+    m.load_state_dict(sd)
+    assert m.lista_blocks[0] is m.lista_blocks[2]
+    assert float(m.lista_blocks[0].Lambda.flatten()[0]) == 7.0
+
+
+def test_cpu_tensors_raise_no_fallback():
+    m = CistaLSTCNet([32, 32], base_channels=32, depth=1, num_bins=5)
+    with torch.no_grad(), pytest.raises(RuntimeError, match="ROCm"):
+        m(torch.zeros(1, 5, 32, 32), torch.zeros(1, 1, 32, 32), None)
+
+
+def test_grad_mode_without_backward_raises():
+    m = CistaLSTCNet([32, 32], base_channels=32, depth=1, num_bins=5)
+    with pytest.raises(RuntimeError, match="backward"):
+        m(torch.zeros(1, 5, 32, 32), torch.zeros(1, 1, 32, 32), None)

@@ -1,0 +1,505 @@
+// cista_kernels.hpp -- device code of the MI355X (gfx950) CISTA-LSTC hot path.
+//
+// One reflect-padded 3x3 implicit-GEMM convolution kernel family does all 18 MFMA-shaped
+// convolutions of a frame (reference e2v/base_layers.py ConvLayer :135-161, ConvLSTC :38-71,
+// ConvLSTM :75-130, UpsampleConvLayer :166-210).  Design:
+//
+//  * activations are NHWC fp32 in HBM; a workgroup owns a TH x TW spatial tile of one sample
+//    and a slice of output channels; the reflect-padded input halo tile of a 32-channel
+//    K-chunk is staged into LDS as split-bf16 (x = hi + lo), so every input element is
+//    fetched from HBM/L2 once per chunk and re-used by 9 taps x all output channels;
+//  * each product a*w is formed as hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_f16 with
+//    fp32 accumulation ("split3-f16"): x = hi + lo with fp16 parts represents an fp32 value to
+//    ~2^-22 relative (absolute 2^-25 below the fp16 normal range), so the three products carry
+//    ~fp32 accuracy: 3e-6 vs the fp64 truth on the stress fixture's LSTM state, where a
+//    bf16 split measured 1.5e-4.  Weights are pre-scaled by a per-layer
+//    power of two so their lo part stays normal; the epilogue undoes it exactly.
+//    Activations must satisfy |x| < 65504 (fp16 range); larger values surface as inf/NaN;
+//  * weights are pre-packed once per parameter update into per-lane MFMA B fragments
+//    (hi and lo), read straight from L2 into VGPRs with 1 KiB coalesced loads;
+//  * every elementwise op of the reference (bias, ReLU, sigmoid/tanh gate algebra, the
+//    LSTC/LSTM cell updates, x1 - D(z), softshrink) is fused into the conv epilogue; gate
+//    columns are permuted at pack time so one lane holds all gates of its (pixel, channel);
+//  * bilinear x2 upsampling + ReflectionPad2d(1) is computed on the fly while staging the
+//    upsample conv's input tile; the stride-2 W0 conv stages a (2TH+1) x (2TW+1) halo.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace cista {
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2 };
+enum Epi {
+    EPI_BIAS = 0,        // out = acc + b
+    EPI_RELU = 1,        // out = relu(acc + b)
+    EPI_ISTA_D = 2,      // out = x1 - (acc + b)                        (e2v_model.py:73-74)
+    EPI_ISTA_P = 3,      // z = softshrink((acc + b) + z, lambda)       (e2v_model.py:75-77)
+    EPI_LSTC_CELL = 4,   // c = sig(f) c_prev + sig(i) z0               (base_layers.py:57-67)
+    EPI_LSTC_OUT = 5,    // z = sig(o) tanh(c)                          (base_layers.py:63,69)
+    EPI_LSTM = 6         // c = sig(r) c_prev + sig(i) tanh(g); h = sig(o) tanh(c) (:112-128)
+};
+
+struct ConvArgs {
+    const float *in0;    // input segment 0, NHWC, c0 channels
+    const float *in1;    // input segment 1, NHWC, c1 channels (NULL => zeros, chunks skipped)
+    int c0, c1;
+    int B, Hin, Win;     // input spatial dims (STAGE_UP: the half-res source)
+    int Hout, Wout;
+    int TH, TW, tiles_x, tiles_y;
+    const u32x4 *wpack;  // [kc][tap][ntile][part][lane] 16-B B fragments
+    const float *bias;   // packed-column order, N entries
+    const float *wscale; // [1]: inverse of the power-of-two weight pre-scale of this layer
+    int N;               // packed output columns (all gates)
+    int Cout;            // channels of each output tensor (N / G)
+    float *out0;         // primary output (NHWC, Cout channels)
+    float *out1;         // secondary output (EPI_LSTM: c)
+    const float *aux0;   // epilogue input 0 (x1 / z_old / c_prev / c)
+    const float *aux1;   // epilogue input 1 (z0)
+    const float *lambda; // EPI_ISTA_P: per-channel threshold
+};
+
+__device__ __forceinline__ int reflect_clamp(int i, int n) {
+    // padding_mode='reflect' with pad 1: -1 -> 1, n -> n-2; tiles overhanging the image by
+    // more than one pixel only feed masked outputs, so clamp keeps those reads in bounds.
+    i = i < 0 ? -i : i;
+    i = i >= n ? 2 * n - 2 - i : i;
+    i = i < 0 ? 0 : i;
+    return i > n - 1 ? n - 1 : i;
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25)
+__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo) {
+    float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+    f16x8 h, l;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 hb = (_Float16)v[i];
+        h[i] = hb;
+        l[i] = (_Float16)(v[i] - (float)hb);
+    }
+    hi = __builtin_bit_cast(u32x4, h);
+    lo = __builtin_bit_cast(u32x4, l);
+}
+
+// ------------------------------------------------------------------------------------------
+// Staging of one 32-channel K-chunk of the halo tile into LDS.
+// LDS image (u32x4 units): [part hi/lo][kgroup 0..3 (8 channels)][HPpad halo pixels]
+// ------------------------------------------------------------------------------------------
+template <int STAGE>
+__device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
+                                            int ix0, int HH, int HWd, int HPpad,
+                                            const float *seg, int segC, int choff) {
+    const int HP = HH * HWd;
+    const int nitems = HP * 4;
+    for (int it = threadIdx.x; it < nitems; it += blockDim.x) {
+        const int g = it & 3;
+        const int hp = it >> 2;
+        const int hy = hp / HWd;
+        const int hx = hp - hy * HWd;
+        float4 v0, v1;
+        if constexpr (STAGE == STAGE_UP) {
+            // virtual input = ReflectionPad2d(1)(interpolate(h, 2x, bilinear, align_corners=False))
+            const int Hu = 2 * a.Hin, Wu = 2 * a.Win;
+            const int Y = reflect_clamp(iy0 + hy, Hu);
+            const int X = reflect_clamp(ix0 + hx, Wu);
+            float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
+            float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
+            const int y0 = (int)sy, x0 = (int)sx;
+            const int y1 = y0 + (y0 < a.Hin - 1 ? 1 : 0);
+            const int x1 = x0 + (x0 < a.Win - 1 ? 1 : 0);
+            const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1;
+            const float lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+            const size_t rowstride = (size_t)a.Win * segC;
+            const float *base = seg + (size_t)b * a.Hin * rowstride + choff + g * 8;
+            const float *p00 = base + (size_t)y0 * rowstride + (size_t)x0 * segC;
+            const float *p01 = base + (size_t)y0 * rowstride + (size_t)x1 * segC;
+            const float *p10 = base + (size_t)y1 * rowstride + (size_t)x0 * segC;
+            const float *p11 = base + (size_t)y1 * rowstride + (size_t)x1 * segC;
+            float r[8];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const float4 a00 = *(const float4 *)(p00 + 4 * h);
+                const float4 a01 = *(const float4 *)(p01 + 4 * h);
+                const float4 a10 = *(const float4 *)(p10 + 4 * h);
+                const float4 a11 = *(const float4 *)(p11 + 4 * h);
+                // torch order: h0l*(w0l*x00 + w1l*x01) + h1l*(w0l*x10 + w1l*x11)
+                r[4 * h + 0] = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
+                r[4 * h + 1] = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
+                r[4 * h + 2] = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
+                r[4 * h + 3] = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
+            }
+            v0 = make_float4(r[0], r[1], r[2], r[3]);
+            v1 = make_float4(r[4], r[5], r[6], r[7]);
+        } else {
+            const int iy = reflect_clamp(iy0 + hy, a.Hin);
+            const int ix = reflect_clamp(ix0 + hx, a.Win);
+            const float *p = seg + (((size_t)b * a.Hin + iy) * a.Win + ix) * segC + choff + g * 8;
+            v0 = *(const float4 *)p;
+            v1 = *(const float4 *)(p + 4);
+        }
+        u32x4 hi, lo;
+        split8(v0, v1, hi, lo);
+        smem[g * HPpad + hp] = hi;
+        smem[(4 + g) * HPpad + hp] = lo;
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
+// MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
+// ------------------------------------------------------------------------------------------
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G>
+__global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
+    static_assert(WM * WN == 4, "4 waves per workgroup");
+    static_assert(NW % G == 0, "a wave must hold whole gate groups");
+    extern __shared__ u32x4 smem[];
+
+    const int lane = threadIdx.x & 63;
+    const int wave = threadIdx.x >> 6;
+    const int wm = wave % WM;
+    const int wn = wave / WM;
+    const int nblk = blockIdx.y;
+
+    int t = blockIdx.x;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    const int b = t / a.tiles_y;
+    const int oy0 = ty * a.TH, ox0 = tx * a.TW;
+
+    constexpr int S = (STAGE == STAGE_S2) ? 2 : 1;
+    const int HWd = (a.TW - 1) * S + 3;
+    const int HH = (a.TH - 1) * S + 3;
+    const int HPpad = (HH * HWd + 15) & ~15;
+    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+    const int Hsrc = (STAGE == STAGE_UP) ? 2 * a.Hin : a.Hin;
+    (void)Hsrc;
+
+    // per-lane A-fragment base (u32x4 units) of every m-tile, tap (0,0)
+    const int npix = a.TH * a.TW;
+    const int kgrp = lane >> 4;
+    int abase[MT_W];
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m) {
+        int p = (wm * MT_W + m) * 16 + (lane & 15);
+        p = p < npix ? p : npix - 1;
+        const int py = p / a.TW;
+        const int px = p - py * a.TW;
+        abase[m] = kgrp * HPpad + py * S * HWd + px * S;
+    }
+
+    f32x4 acc[MT_W][NW];
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+        for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+    const int NT = a.N >> 4;
+    const int nt0 = (nblk * WN + wn) * NW;
+    const int kc0 = a.c0 >> 5;
+    const int nchunks = kc0 + (a.in1 ? (a.c1 >> 5) : 0);
+    const size_t tapstride = (size_t)NT * 2 * 64;   // u32x4 per tap
+
+    for (int kc = 0; kc < nchunks; ++kc) {
+        const float *seg = kc < kc0 ? a.in0 : a.in1;
+        const int segC = kc < kc0 ? a.c0 : a.c1;
+        const int choff = (kc < kc0 ? kc : kc - kc0) * 32;
+        __syncthreads();
+        stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff);
+        __syncthreads();
+
+        const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
+#pragma unroll 1
+        for (int tap = 0; tap < 9; ++tap) {
+            u32x4 bh[NW], bl[NW];
+            const u32x4 *wq = wp + (size_t)tap * tapstride;
+#pragma unroll
+            for (int n = 0; n < NW; ++n) {
+                bh[n] = wq[n * 128];
+                bl[n] = wq[n * 128 + 64];
+            }
+            const int toff = (tap / 3) * HWd + (tap % 3);
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) {
+                const f16x8 ah = __builtin_bit_cast(f16x8, smem[abase[m] + toff]);
+                const f16x8 al = __builtin_bit_cast(f16x8, smem[4 * HPpad + abase[m] + toff]);
+#pragma unroll
+                for (int n = 0; n < NW; ++n) {
+                    const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
+                    const f16x8 wl = __builtin_bit_cast(f16x8, bl[n]);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl, acc[m][n], 0, 0, 0);
+                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh, acc[m][n], 0, 0, 0);
+                }
+            }
+        }
+    }
+
+    // ---------------------------------- epilogue ----------------------------------------
+    // acc[m][n][j]: pixel row (wm*MT_W+m)*16 + 4*(lane>>4) + j, packed column (nt0+n)*16 + lane&15
+    const int col = lane & 15;
+    const float ws = *a.wscale;
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+        for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
+            if (p >= npix) continue;
+            const int py = p / a.TW;
+            const int px = p - py * a.TW;
+            const int oy = oy0 + py, ox = ox0 + px;
+            if (oy >= a.Hout || ox >= a.Wout) continue;
+            const size_t pix = ((size_t)b * a.Hout + oy) * a.Wout + ox;
+            if constexpr (G == 1) {
+#pragma unroll
+                for (int n = 0; n < NW; ++n) {
+                    const int ch = (nt0 + n) * 16 + col;
+                    float v = acc[m][n][j] + a.bias[ch];
+                    const size_t o = pix * a.Cout + ch;
+                    if constexpr (EPI == EPI_RELU) {
+                        v = fmaxf(v, 0.0f);
+                    } else if constexpr (EPI == EPI_ISTA_D) {
+                        v = a.aux0[o] - v;
+                    } else if constexpr (EPI == EPI_ISTA_P) {
+                        const float x = v + a.aux0[o];
+                        const float lam = a.lambda[ch];
+                        v = fmaxf(x - lam, 0.0f) - fmaxf(-x - lam, 0.0f);
+                    } else if constexpr (EPI == EPI_LSTC_OUT) {
+                        v = sigmoidf_(v) * tanhf(a.aux0[o]);
+                    }
+                    a.out0[o] = v;
+                }
+            } else {
+#pragma unroll
+                for (int q = 0; q < NW / G; ++q) {
+                    const int cblk = (nt0 / G) + q;
+                    const int ch = cblk * 16 + col;           // channel within one gate
+                    const size_t o = pix * a.Cout + ch;
+                    if constexpr (EPI == EPI_LSTC_CELL) {
+                        // packed n-tile order per channel block: (in, forget)
+                        const float gi = sigmoidf_(acc[m][q * 2 + 0][j] + a.bias[(nt0 + q * 2 + 0) * 16 + col]);
+                        const float gf = sigmoidf_(acc[m][q * 2 + 1][j] + a.bias[(nt0 + q * 2 + 1) * 16 + col]);
+                        const float cp = a.aux0 ? a.aux0[o] : 0.0f;
+                        a.out0[o] = gf * cp + gi * a.aux1[o];
+                    } else if constexpr (EPI == EPI_LSTM) {
+                        // packed n-tile order per channel block: (in, remember, out, cell)
+                        const float gi = sigmoidf_(acc[m][q * 4 + 0][j] + a.bias[(nt0 + q * 4 + 0) * 16 + col]);
+                        const float gr = sigmoidf_(acc[m][q * 4 + 1][j] + a.bias[(nt0 + q * 4 + 1) * 16 + col]);
+                        const float go = sigmoidf_(acc[m][q * 4 + 2][j] + a.bias[(nt0 + q * 4 + 2) * 16 + col]);
+                        const float gc = tanhf(acc[m][q * 4 + 3][j] + a.bias[(nt0 + q * 4 + 3) * 16 + col]);
+                        const float cp = a.aux0 ? a.aux0[o] : 0.0f;
+                        const float c = gr * cp + gi * gc;
+                        a.out0[o] = go * tanhf(c);
+                        a.out1[o] = c;
+                    }
+                }
+            }
+        }
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Input stage: x_full (B,H,W,C) NHWC = cat(We(events), Wi(prev_image))   (e2v_model.py:62-64)
+// VALU: 0.3 % of the frame's FLOPs.  Thread = (pixel, 16 output channels).
+// ------------------------------------------------------------------------------------------
+struct InputArgs {
+    const float *events;   // (B, nb, H, W)
+    const float *prev;     // (B, 1, H, W)
+    const float *wE;       // [nb*9][C/2]  (cin, tap) major
+    const float *wI;       // [9][C/2]
+    const float *bias;     // [C]  (We then Wi)
+    float *out;            // (B, H, W, C)
+    int B, H, W, nb, C;
+};
+
+__global__ __launch_bounds__(256) void input_stage_kernel(const InputArgs a) {
+    const int groups = a.C / 16;
+    const long total = (long)a.B * a.H * a.W * groups;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int g = (int)(idx % groups);
+    const long pix = idx / groups;
+    const int x = (int)(pix % a.W);
+    const int y = (int)((pix / a.W) % a.H);
+    const int b = (int)(pix / ((long)a.W * a.H));
+    const int half = a.C / 2;
+    const bool isE = g < groups / 2;
+    const int cbase = (isE ? g : g - groups / 2) * 16;
+    float acc[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) acc[i] = 0.0f;
+    int ys[3], xs[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        ys[d] = reflect_clamp(y + d - 1, a.H);
+        xs[d] = reflect_clamp(x + d - 1, a.W);
+    }
+    const size_t plane = (size_t)a.H * a.W;
+    if (isE) {
+        for (int ci = 0; ci < a.nb; ++ci) {
+            const float *src = a.events + ((size_t)b * a.nb + ci) * plane;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float v = src[(size_t)ys[t / 3] * a.W + xs[t % 3]];
+                const float *w = a.wE + (size_t)(ci * 9 + t) * half + cbase;
+#pragma unroll
+                for (int i = 0; i < 16; ++i) acc[i] = fmaf(v, w[i], acc[i]);
+            }
+        }
+    } else {
+        const float *src = a.prev + (size_t)b * plane;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float v = src[(size_t)ys[t / 3] * a.W + xs[t % 3]];
+            const float *w = a.wI + (size_t)t * half + cbase;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = fmaf(v, w[i], acc[i]);
+        }
+    }
+    const int och = (isE ? 0 : half) + cbase;
+    float4 *o = (float4 *)(a.out + (size_t)pix * a.C + och);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        o[i] = make_float4(acc[4 * i] + a.bias[och + 4 * i], acc[4 * i + 1] + a.bias[och + 4 * i + 1],
+                           acc[4 * i + 2] + a.bias[och + 4 * i + 2], acc[4 * i + 3] + a.bias[och + 4 * i + 3]);
+}
+
+// ------------------------------------------------------------------------------------------
+// Final stage: rec = sigmoid(final_conv(u)), u (B,H,W,C) NHWC            (e2v_model.py:87-88)
+// One wave per 64 pixels; each lane reduces its pixel over 9 taps x C channels.
+// ------------------------------------------------------------------------------------------
+struct FinalArgs {
+    const float *u;      // (B,H,W,C)
+    const float *w;      // [9][C]
+    const float *bias;   // [1]
+    float *rec;          // (B,1,H,W)
+    float *pre;          // optional pre-sigmoid
+    int B, H, W, C;
+};
+
+__global__ __launch_bounds__(256) void final_stage_kernel(const FinalArgs a) {
+    const long total = (long)a.B * a.H * a.W;
+    const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= total) return;
+    const int x = (int)(pix % a.W);
+    const int y = (int)((pix / a.W) % a.H);
+    const int b = (int)(pix / ((long)a.W * a.H));
+    float acc = 0.0f;
+    for (int t = 0; t < 9; ++t) {
+        const int yy = reflect_clamp(y + t / 3 - 1, a.H);
+        const int xx = reflect_clamp(x + t % 3 - 1, a.W);
+        const float4 *src = (const float4 *)(a.u + (((size_t)b * a.H + yy) * a.W + xx) * a.C);
+        const float4 *w = (const float4 *)(a.w + (size_t)t * a.C);
+        for (int c4 = 0; c4 < a.C / 4; ++c4) {
+            const float4 v = src[c4];
+            const float4 k = w[c4];
+            acc = fmaf(v.x, k.x, acc);
+            acc = fmaf(v.y, k.y, acc);
+            acc = fmaf(v.z, k.z, acc);
+            acc = fmaf(v.w, k.w, acc);
+        }
+    }
+    const float pre = acc + a.bias[0];
+    if (a.pre) a.pre[pix] = pre;
+    a.rec[pix] = sigmoidf_(pre);
+}
+
+// ------------------------------------------------------------------------------------------
+// Weight packing (once per parameter update).
+// ------------------------------------------------------------------------------------------
+struct PackArgs {
+    const float *w;      // [Cout][Cin][3][3]
+    const float *b;      // [Cout]
+    float *scale;        // [2]: {pre-scale s, 1/s}, written by weight_scale_kernel
+    u32x4 *wp;           // [kc][tap][nt][part][lane]
+    float *bp;           // [N] packed-column bias
+    int Cout, Cin, G;    // G: gates grouped per channel block
+};
+
+__device__ __forceinline__ int packed_col_to_cout(int pc, int N, int G) {
+    const int nt = pc >> 4, r = pc & 15;
+    const int g = nt % G, cblk = nt / G;
+    return g * (N / G) + cblk * 16 + r;
+}
+
+__global__ void pack_conv_kernel(const PackArgs a) {
+    const int NT = a.Cout / 16;
+    const int KC = a.Cin / 32;
+    const long total = (long)KC * 9 * NT * 64;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < a.Cout) a.bp[idx] = a.b[packed_col_to_cout((int)idx, a.Cout, a.G)];
+    if (idx >= total) return;
+    const int lane = (int)(idx % 64);
+    long r = idx / 64;
+    const int nt = (int)(r % NT);
+    r /= NT;
+    const int tap = (int)(r % 9);
+    const int kc = (int)(r / 9);
+    const int cout = packed_col_to_cout(nt * 16 + (lane & 15), a.Cout, a.G);
+    const float s = a.scale[0];
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int cin = kc * 32 + 8 * (lane >> 4) + j;
+        const float v = a.w[((size_t)cout * a.Cin + cin) * 9 + tap] * s;   // exact (2^e)
+        const _Float16 hb = (_Float16)v;
+        h[j] = hb;
+        l[j] = (_Float16)(v - (float)hb);
+    }
+    const size_t base = ((((size_t)kc * 9 + tap) * NT + nt) * 2) * 64 + lane;
+    a.wp[base] = __builtin_bit_cast(u32x4, h);
+    a.wp[base + 64] = __builtin_bit_cast(u32x4, l);
+}
+
+// Per-layer power-of-two pre-scale: s = 2^floor(log2(16384 / max|w|)), clamped to 2^[-24, 40],
+// so w*s stays well inside fp16 range and its lo part stays a normal fp16 number.
+__global__ __launch_bounds__(1024) void weight_scale_kernel(const float *w, long n, float *scale) {
+    __shared__ float red[1024];
+    float m = 0.0f;
+    for (long i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int s = 512; s > 0; s >>= 1) {
+        if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        const float mx = red[0];
+        int e = 0;
+        if (mx > 0.0f && isfinite(mx)) {
+            e = (int)floorf(log2f(16384.0f / mx));
+            e = e < -24 ? -24 : (e > 40 ? 40 : e);
+        }
+        scale[0] = ldexpf(1.0f, e);
+        scale[1] = ldexpf(1.0f, -e);
+    }
+}
+
+// final_conv weight [1][C][3][3] -> [tap][C] fp32
+__global__ void final_weight_kernel(const float *w, float *o, int C) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C * 9) return;
+    const int c = idx % C, t = idx / C;
+    o[idx] = w[c * 9 + t];
+}
+
+// We/Wi weights: [Cout][Cin][3][3] -> [(cin*9+tap)][Cout] fp32
+__global__ void transpose_small_kernel(const float *w, float *o, int Cout, int Cin) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= Cout * Cin * 9) return;
+    const int co = idx % Cout;
+    const int k = idx / Cout;   // cin*9 + tap
+    o[idx] = w[(size_t)co * Cin * 9 + k];
+}
+
+}  // namespace cista

@@ -1,0 +1,173 @@
+"""CistaLSTCNet -- drop-in for reference e2v/e2v_model.py:5-90, computed by libcista_hip.so.
+
+Same constructor, same ``forward(events, prev_image, prev_states) -> (rec_I, states)``, same
+45-key ``state_dict`` (so reference ``.pth.tar`` checkpoints load with ``strict=True``).
+``test_e2v.py`` / ``model_v2e2v.py`` only need ``from v2e2v_amd import CistaLSTCNet``
+(INTEGRATION.md).
+
+Differences a caller can observe (all documented in DESIGN.md):
+* the returned recurrent states are ``torch.channels_last`` tensors -- identical shapes and
+  values, NHWC strides (the kernels' native layout, so no per-frame transposes); states of
+  any layout are accepted back;
+* the path runs on ROCm devices only; CPU tensors raise (the CPU restatement lives in
+  ``oracle/`` and is test infrastructure, never a fallback);
+* numerics: convolutions use the split-bf16 3-pass MFMA scheme (fp32 accumulate); results
+  match the reference fp32 CPU path within 1e-4 (tests/test_gpu_parity.py).
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+
+from . import _lib
+from .base_layers import ConvLayer, ConvLSTC, IstaBlock, RecurrentConvLayer, UpsampleConvLayer
+
+
+class CistaLSTCNet(nn.Module):
+    def __init__(self, image_dim, base_channels=64, depth=5, num_bins=5):
+        super().__init__()
+        self.num_bins = num_bins
+        self.depth = depth
+        self.height, self.width = image_dim          # stored, unused (reference :13)
+        self.num_states = 3
+        self.base_channels = base_channels
+        C = base_channels
+        # construction order == reference e2v_model.py:17-38 (same RNG draws)
+        self.We = ConvLayer(num_bins, int(C / 2), 3, stride=1, padding=1)
+        self.Wi = ConvLayer(1, int(C / 2), 3, stride=1, padding=1)
+        self.W0 = ConvLayer(C, C, 3, stride=2, padding=1)
+        self.P0 = ConvLSTC(x_size=C, z_size=2 * C, output_size=2 * C, kernel_size=3)
+        lista_block = IstaBlock(base_channels=C)
+        self.lista_blocks = nn.ModuleList([lista_block for _ in range(depth)])   # tied
+        self.Dg = RecurrentConvLayer(2 * C, C, kernel_size=3, stride=1, padding=1,
+                                     activation="relu")
+        self.upsamp_conv = UpsampleConvLayer(C, C, kernel_size=3, stride=1, padding=0,
+                                             activation="relu")
+        self.final_conv = ConvLayer(C, 1, 3, stride=1, padding=1)
+        self.sigmoid = nn.Sigmoid()
+        self._packed = None
+        self._packed_key = None
+        self._ws = None
+
+    # ------------------------------------------------------------------ internals
+    def _cfg(self):
+        return _lib.CistaConfig(self.base_channels, self.depth, self.num_bins)
+
+    def _unique_params(self):
+        blk = self.lista_blocks[0] if self.depth > 0 else None
+        if blk is None:
+            raise RuntimeError("depth=0 has no IstaBlock parameters")
+        return [
+            self.We.conv2d.weight, self.We.conv2d.bias, self.Wi.conv2d.weight, self.Wi.conv2d.bias,
+            self.W0.conv2d.weight, self.W0.conv2d.bias, self.P0.gates.weight, self.P0.gates.bias,
+            self.P0.out_gates.weight, self.P0.out_gates.bias, self.P0.P0.weight, self.P0.P0.bias,
+            blk.Lambda, blk.D.conv2d.weight, blk.D.conv2d.bias, blk.P.conv2d.weight,
+            blk.P.conv2d.bias, self.Dg.conv.conv2d.weight, self.Dg.conv.conv2d.bias,
+            self.Dg.recurrent_block.Gates.weight, self.Dg.recurrent_block.Gates.bias,
+            self.upsamp_conv.conv2d.weight, self.upsamp_conv.conv2d.bias,
+            self.final_conv.conv2d.weight, self.final_conv.conv2d.bias,
+        ]
+
+    def packed_params(self):
+        """Split-bf16 MFMA tiles of the current parameters; repacked whenever any parameter
+        changed (load_state_dict, optimizer step: tracked through tensor versions)."""
+        params = self._unique_params()
+        dev = params[0].device
+        if dev.type != "cuda":
+            raise RuntimeError("CistaLSTCNet (MI355X build) runs on ROCm devices only; move the "
+                               "module to 'cuda' (the CPU restatement is test-only: oracle/)")
+        key = tuple((p.data_ptr(), p._version) for p in params)
+        if self._packed is not None and self._packed_key == key:
+            return self._packed
+        L = _lib.lib()
+        cfg = self._cfg()
+        nbytes = L.cista_packed_bytes(ctypes_ref(cfg))
+        packed = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+        contig = [p.detach().float().contiguous() for p in params]
+        cp = _lib.CistaParams(*[t.data_ptr() for t in contig])
+        _lib.check(L.cista_pack_params(ctypes_ref(cfg), ctypes_ref(cp), packed.data_ptr(),
+                                       _lib.stream_handle(dev)), "cista_pack_params")
+        self._contig_keepalive = contig     # keep sources alive until the pack kernels ran
+        self._packed, self._packed_key = packed, key
+        return packed
+
+    def workspace(self, B, H, W, device):
+        L = _lib.lib()
+        n = L.cista_workspace_bytes(ctypes_ref(self._cfg()), B, H, W)
+        if self._ws is None or self._ws.numel() < n or self._ws.device != device:
+            self._ws = torch.empty(n, dtype=torch.uint8, device=device)
+        return self._ws
+
+    # ------------------------------------------------------------------ forward
+    def forward(self, events, prev_image, prev_states):
+        """reference e2v/e2v_model.py:41-90.  events (B,nb,H,W), prev_image (B,1,H,W),
+        prev_states None or [c_lstc, z, (h, c)] -> (rec_I (B,1,H,W), [c_lstc, z, (h, c)])."""
+        if torch.is_grad_enabled() and (events.requires_grad or prev_image.requires_grad or
+                                        any(p.requires_grad for p in self.parameters())):
+            raise RuntimeError("CistaLSTCNet (MI355X build): the BPTT backward kernels are not "
+                               "built yet -- run inference under torch.no_grad()")
+        return _forward_frame(self, events, prev_image, prev_states)
+
+
+def ctypes_ref(x):
+    import ctypes
+    return ctypes.byref(x)
+
+
+def _check_input(name, t, shape, device):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor")
+    if tuple(t.shape) != tuple(shape):
+        raise RuntimeError(f"{name}: expected shape {tuple(shape)}, got {tuple(t.shape)}")
+    if t.device != device:
+        raise RuntimeError(f"{name} is on {t.device}, the model is on {device}")
+
+
+def _state(t, shape, device, name):
+    if t is None:
+        return None
+    _check_input(name, t, shape, device)
+    return t.detach().float().contiguous(memory_format=torch.channels_last)
+
+
+def _forward_frame(model, events, prev_image, prev_states):
+    packed = model.packed_params()
+    dev = packed.device
+    if events.dim() != 4:
+        raise RuntimeError(f"events must be (B, num_bins, H, W), got {tuple(events.shape)}")
+    B, nb, H, W = events.shape
+    C = model.base_channels
+    if nb != model.num_bins:
+        raise RuntimeError(f"events has {nb} bins, model expects num_bins={model.num_bins}")
+    if H % 2 or W % 2:
+        raise RuntimeError(f"H and W must be even (reference upsampling needs it), got {H}x{W}")
+    _check_input("events", events, (B, nb, H, W), dev)
+    _check_input("prev_image", prev_image, (B, 1, H, W), dev)
+    h, w = H // 2, W // 2
+    if prev_states is None:
+        prev_states = [None] * model.num_states
+    c_lstc_p = _state(prev_states[0], (B, 2 * C, h, w), dev, "prev_states[0]")
+    z_p = _state(prev_states[-2], (B, 2 * C, h, w), dev, "prev_states[1]")
+    hc = prev_states[-1]
+    if hc is None:
+        h_p = c_p = None
+    else:
+        h_p = _state(hc[0], (B, C, h, w), dev, "prev_states[2][0]")
+        c_p = _state(hc[1], (B, C, h, w), dev, "prev_states[2][1]")
+    ev = events.detach().float().contiguous()
+    pi = prev_image.detach().float().contiguous()
+    cl = torch.channels_last
+    rec = torch.empty(B, 1, H, W, device=dev, dtype=torch.float32)
+    c_lstc = torch.empty(B, 2 * C, h, w, device=dev, dtype=torch.float32, memory_format=cl)
+    z = torch.empty(B, 2 * C, h, w, device=dev, dtype=torch.float32, memory_format=cl)
+    hs = torch.empty(B, C, h, w, device=dev, dtype=torch.float32, memory_format=cl)
+    cs = torch.empty(B, C, h, w, device=dev, dtype=torch.float32, memory_format=cl)
+    ws = model.workspace(B, H, W, dev)
+    P = _lib.ptr
+    io = _lib.CistaFrameIO(P(ev), P(pi), P(c_lstc_p), P(z_p), P(h_p), P(c_p),
+                           P(rec), P(c_lstc), P(z), P(hs), P(cs))
+    L = _lib.lib()
+    _lib.check(L.cista_forward(ctypes_ref(model._cfg()), packed.data_ptr(), B, H, W,
+                               ctypes_ref(io), ws.data_ptr(), ws.numel(),
+                               _lib.stream_handle(dev)), "cista_forward")
+    return rec, [c_lstc, z, (hs, cs)]
