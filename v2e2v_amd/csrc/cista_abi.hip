@@ -133,6 +133,18 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S) {
     return best;
 }
 
+// dynamic LDS above 64 KiB must be enabled per kernel (once; not a stream operation)
+bool allow_big_lds(const void *kern) {
+    static const void *done[64];
+    static int ndone = 0;
+    for (int i = 0; i < ndone; ++i)
+        if (done[i] == kern) return true;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+        return false;
+    if (ndone < 64) done[ndone++] = kern;
+    return true;
+}
+
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
@@ -148,13 +160,7 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int nblk_cols = WN * NW * 16;
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
     auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G>;
-    static bool attr_done = false;
-    if (!attr_done) {
-        if (hipFuncSetAttribute((const void *)kern, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                160 * 1024) != hipSuccess)
-            return CISTA_ERR_HIP;
-        attr_done = true;
-    }
+    if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
     hipLaunchKernelGGL(kern, grid, dim3(256), t.lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
@@ -166,6 +172,10 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
         if (a.N % 64 == 0) return launch_conv_cfg<2, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N % 32 == 0) return launch_conv_cfg<2, 2, 4, 1, STAGE, EPI, G>(a, st);
+        return CISTA_ERR_UNSUPPORTED;
+    } else if constexpr (EPI == EPI_UP_Q) {      // needs WN == 1
+        if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
+        if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
     } else {
         if (a.N >= 256 && a.N % 256 == 0) return launch_conv_cfg<8, 4, 1, 4, STAGE, EPI, G>(a, st);
@@ -225,6 +235,9 @@ struct Frame {
     hipStream_t st;
 };
 
+// the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
+inline bool up_q_path(int C) { return C == 64 || C == 32; }
+
 int run_layer(const Frame &f, int layer) {
     const int C = f.C, B = f.B, h = f.h, w = f.w;
     ConvArgs a;
@@ -235,9 +248,23 @@ int run_layer(const Frame &f, int layer) {
             ia.wE = blob<float>(f.packed, f.L.wE); ia.wI = blob<float>(f.packed, f.L.wI);
             ia.bias = blob<float>(f.packed, f.L.bIn);
             ia.out = f.full; ia.B = B; ia.H = f.H; ia.W = f.W; ia.nb = f.cfg->num_bins; ia.C = C;
-            const long total = (long)B * f.H * f.W * (C / 16);
-            hipLaunchKernelGGL(input_stage_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
-                               0, f.st, ia);
+            const long npix = (long)B * f.H * f.W;
+            const dim3 g1((unsigned)((npix + 255) / 256));
+            const size_t lds = (size_t)256 * (C + 1) * 4;
+            switch (f.cfg->num_bins) {
+#define NBCASE(n)                                                                           \
+    case n:                                                                                 \
+        if (!allow_big_lds((const void *)input_stage_kernel_nb<n>)) return CISTA_ERR_HIP;  \
+        hipLaunchKernelGGL(input_stage_kernel_nb<n>, g1, dim3(256), lds, f.st, ia);        \
+        break;
+                NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7) NBCASE(8)
+#undef NBCASE
+                default: {
+                    const long total = npix * (C / 16);
+                    hipLaunchKernelGGL(input_stage_kernel, dim3((unsigned)((total + 255) / 256)),
+                                       dim3(256), 0, f.st, ia);
+                }
+            }
             return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
         }
         case CISTA_LAYER_W0:                                           // e2v_model.py:66
@@ -275,14 +302,25 @@ int run_layer(const Frame &f, int layer) {
         case CISTA_LAYER_UPSAMPLE:  // relu(conv(ReflectionPad(up2x(h))))          :193-210
             a = conv_args(f.packed, f.L, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
             a.out0 = f.full;
+            if (up_q_path(C)) {     // + final_conv's channel contraction in the epilogue
+                a.aux0 = blob<float>(f.packed, f.L.wF);
+                return launch_conv<STAGE_UP, EPI_UP_Q, 1>(a, f.st);
+            }
             return launch_conv<STAGE_UP, EPI_RELU, 1>(a, f.st);
         case CISTA_LAYER_FINAL: {   // sigmoid(final_conv(u))                  e2v_model.py:87-88
-            FinalArgs fa;
-            fa.u = f.full; fa.w = blob<float>(f.packed, f.L.wF); fa.bias = blob<float>(f.packed, f.L.bF);
-            fa.rec = f.rec; fa.pre = f.pre; fa.B = B; fa.H = f.H; fa.W = f.W; fa.C = C;
             const long total = (long)B * f.H * f.W;
-            hipLaunchKernelGGL(final_stage_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256),
-                               0, f.st, fa);
+            const dim3 g1((unsigned)((total + 255) / 256));
+            if (up_q_path(C)) {
+                FinalQArgs fq;
+                fq.q = f.full; fq.bias = blob<float>(f.packed, f.L.bF);
+                fq.rec = f.rec; fq.pre = f.pre; fq.B = B; fq.H = f.H; fq.W = f.W;
+                hipLaunchKernelGGL(final_q_kernel, g1, dim3(256), 0, f.st, fq);
+            } else {
+                FinalArgs fa;
+                fa.u = f.full; fa.w = blob<float>(f.packed, f.L.wF); fa.bias = blob<float>(f.packed, f.L.bF);
+                fa.rec = f.rec; fa.pre = f.pre; fa.B = B; fa.H = f.H; fa.W = f.W; fa.C = C;
+                hipLaunchKernelGGL(final_stage_kernel, g1, dim3(256), 0, f.st, fa);
+            }
             return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
         }
         default:

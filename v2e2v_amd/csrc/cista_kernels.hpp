@@ -6,7 +6,7 @@
 //
 //  * activations are NHWC fp32 in HBM; a workgroup owns a TH x TW spatial tile of one sample
 //    and a slice of output channels; the reflect-padded input halo tile of a 32-channel
-//    K-chunk is staged into LDS as split-bf16 (x = hi + lo), so every input element is
+//    K-chunk is staged into LDS as split-fp16 (x = hi + lo), so every input element is
 //    fetched from HBM/L2 once per chunk and re-used by 9 taps x all output channels;
 //  * each product a*w is formed as hi*hi + hi*lo + lo*hi on v_mfma_f32_16x16x32_f16 with
 //    fp32 accumulation ("split3-f16"): x = hi + lo with fp16 parts represents an fp32 value to
@@ -40,7 +40,10 @@ enum Epi {
     EPI_ISTA_P = 3,      // z = softshrink((acc + b) + z, lambda)       (e2v_model.py:75-77)
     EPI_LSTC_CELL = 4,   // c = sig(f) c_prev + sig(i) z0               (base_layers.py:57-67)
     EPI_LSTC_OUT = 5,    // z = sig(o) tanh(c)                          (base_layers.py:63,69)
-    EPI_LSTM = 6         // c = sig(r) c_prev + sig(i) tanh(g); h = sig(o) tanh(c) (:112-128)
+    EPI_LSTM = 6,        // c = sig(r) c_prev + sig(i) tanh(g); h = sig(o) tanh(c) (:112-128)
+    EPI_UP_Q = 7         // u = relu(acc + b) -> q_t = sum_c u_c * wf[t][c], t = 0..8: the
+                         // final_conv (64->1) contracted over channels in the epilogue, so u
+                         // never reaches HBM; the 9 shifted taps are summed by final_q_kernel
 };
 
 struct ConvArgs {
@@ -249,6 +252,57 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     for (int m = 0; m < MT_W; ++m)
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
+
+    if constexpr (EPI == EPI_UP_Q) {
+        static_assert(WN == 1, "the wave must hold every output channel");
+        // values v[t*4 + j] (tap t, accumulator row j) of this lane's channel subset, then a
+        // reduce-scatter over the 16 lanes (columns) of each row group: after halving 48 -> 3,
+        // lane `col` holds the channel sums of value indices 3*col .. 3*col+2.
+        float bz[NW];
+#pragma unroll
+        for (int n = 0; n < NW; ++n) bz[n] = a.bias[(nt0 + n) * 16 + col];
+#pragma unroll
+        for (int m = 0; m < MT_W; ++m) {
+            float v[48];
+#pragma unroll
+            for (int i = 0; i < 48; ++i) v[i] = 0.0f;
+#pragma unroll
+            for (int n = 0; n < NW; ++n) {
+                const float *wf = a.aux0 + (nt0 + n) * 16 + col;
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    const float u = fmaxf(acc[m][n][j] + bz[n], 0.0f);
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) v[t * 4 + j] = fmaf(u, wf[t * a.Cout], v[t * 4 + j]);
+                }
+            }
+#pragma unroll
+            for (int o = 8, half = 24; o >= 1; o >>= 1, half >>= 1) {
+                const bool up = (col & o) != 0;
+#pragma unroll
+                for (int i = 0; i < half; ++i) {
+                    const float keep = up ? v[i + half] : v[i];
+                    const float send = up ? v[i] : v[i + half];
+                    v[i] = keep + __shfl_xor(send, o);
+                }
+            }
+#pragma unroll
+            for (int r = 0; r < 3; ++r) {
+                const int idx = 3 * col + r;
+                if (idx >= 36) continue;
+                const int t = idx >> 2, j = idx & 3;
+                const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
+                if (p >= npix) continue;
+                const int py = p / a.TW;
+                const int px = p - py * a.TW;
+                const int oy = oy0 + py, ox = ox0 + px;
+                if (oy >= a.Hout || ox >= a.Wout) continue;
+                a.out0[(((size_t)b * 9 + t) * a.Hout + oy) * a.Wout + ox] = v[r];
+            }
+        }
+        return;
+    }
+
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
 #pragma unroll
@@ -322,6 +376,7 @@ struct InputArgs {
     int B, H, W, nb, C;
 };
 
+// Generic fallback (any num_bins): thread = (pixel, 16 output channels).
 __global__ __launch_bounds__(256) void input_stage_kernel(const InputArgs a) {
     const int groups = a.C / 16;
     const long total = (long)a.B * a.H * a.W * groups;
@@ -372,6 +427,104 @@ __global__ __launch_bounds__(256) void input_stage_kernel(const InputArgs a) {
     for (int i = 0; i < 4; ++i)
         o[i] = make_float4(acc[4 * i] + a.bias[och + 4 * i], acc[4 * i + 1] + a.bias[och + 4 * i + 1],
                            acc[4 * i + 2] + a.bias[och + 4 * i + 2], acc[4 * i + 3] + a.bias[och + 4 * i + 3]);
+}
+
+// Fast path (NB bins known at compile time): thread = one pixel of a 256-pixel run of the
+// flattened (b, y, x) index; its 9*(NB+1) reflect-padded inputs live in registers, the weights
+// are wave-uniform (scalar loads, SGPR operands), and the 256 x C outputs -- one contiguous
+// 256*C*4-byte run of the NHWC tensor -- leave through an LDS transpose as coalesced float4s.
+template <int NB>
+__global__ __launch_bounds__(256) void input_stage_kernel_nb(const InputArgs a) {
+    extern __shared__ float tile[];           // [256][C + 1]
+    const int C = a.C, half = C / 2, ld = C + 1;
+    const long total = (long)a.B * a.H * a.W;
+    const long pix0 = (long)blockIdx.x * 256;
+    const long pix = pix0 + threadIdx.x;
+    const bool live = pix < total;
+    const long pc = live ? pix : total - 1;
+    const int x = (int)(pc % a.W);
+    const int y = (int)((pc / a.W) % a.H);
+    const int b = (int)(pc / ((long)a.W * a.H));
+    int off[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t)
+        off[t] = reflect_clamp(y + t / 3 - 1, a.H) * a.W + reflect_clamp(x + t % 3 - 1, a.W);
+    const size_t plane = (size_t)a.H * a.W;
+    float ev[NB * 9], im[9];
+#pragma unroll
+    for (int ci = 0; ci < NB; ++ci)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) ev[ci * 9 + t] = a.events[((size_t)b * NB + ci) * plane + off[t]];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) im[t] = a.prev[(size_t)b * plane + off[t]];
+    float *row = tile + threadIdx.x * ld;
+    for (int c0 = 0; c0 < half; c0 += 16) {
+        float acc[16], acc2[16];
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            acc[i] = a.bias[c0 + i];
+            acc2[i] = a.bias[half + c0 + i];
+        }
+#pragma unroll
+        for (int k = 0; k < NB * 9; ++k) {
+            const float *w = a.wE + (size_t)k * half + c0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc[i] = fmaf(ev[k], w[i], acc[i]);
+        }
+#pragma unroll
+        for (int t = 0; t < 9; ++t) {
+            const float *w = a.wI + (size_t)t * half + c0;
+#pragma unroll
+            for (int i = 0; i < 16; ++i) acc2[i] = fmaf(im[t], w[i], acc2[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            row[c0 + i] = acc[i];
+            row[half + c0 + i] = acc2[i];
+        }
+    }
+    __syncthreads();
+    const long nvalid = (total - pix0) < 256 ? (total - pix0) : 256;
+    const int nf4 = (int)(nvalid * C / 4);
+    float4 *dst = (float4 *)(a.out + (size_t)pix0 * C);
+    for (int i = threadIdx.x; i < nf4; i += 256) {
+        const int e = i * 4;
+        const int p = e / C, c = e - p * C;
+        const float *srow = tile + p * ld + c;
+        dst[i] = make_float4(srow[0], srow[1], srow[2], srow[3]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Final stage (q path): rec = sigmoid(b + sum_t q_t(reflect(y+dy), reflect(x+dx)))   (:87-88)
+// q = (B, 9, H, W) per-tap channel contractions written by the EPI_UP_Q epilogue.
+// ------------------------------------------------------------------------------------------
+struct FinalQArgs {
+    const float *q;      // (B, 9, H, W)
+    const float *bias;   // [1]
+    float *rec;          // (B,1,H,W)
+    float *pre;          // optional pre-sigmoid
+    int B, H, W;
+};
+
+__global__ __launch_bounds__(256) void final_q_kernel(const FinalQArgs a) {
+    const long total = (long)a.B * a.H * a.W;
+    const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= total) return;
+    const int x = (int)(pix % a.W);
+    const int y = (int)((pix / a.W) % a.H);
+    const int b = (int)(pix / ((long)a.W * a.H));
+    const size_t plane = (size_t)a.H * a.W;
+    const float *q = a.q + (size_t)b * 9 * plane;
+    float acc = a.bias[0];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        const int yy = reflect_clamp(y + t / 3 - 1, a.H);
+        const int xx = reflect_clamp(x + t % 3 - 1, a.W);
+        acc += q[t * plane + (size_t)yy * a.W + xx];
+    }
+    if (a.pre) a.pre[pix] = acc;
+    a.rec[pix] = sigmoidf_(acc);
 }
 
 // ------------------------------------------------------------------------------------------
