@@ -17,11 +17,16 @@ for step in "$@"; do
       rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.err; [ $rc -eq 0 ] || exit $rc ;;
+    list)
+      timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; echo "list rc=$?" ;;
+    sq)
+      timeout -k 10 600 rocprofv3 --pmc ${SQ_CTRS:-SQ_WAVES SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_VALU_MFMA_BUSY_CYCLES SQ_LDS_BANK_CONFLICT} --kernel-trace -f csv -d gpurun_out/pmc_sq -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --layer-reps 3 > /dev/null 2> gpurun_out/pmc_sq.err
+      rc=$?; echo "sq rc=$rc"; tail -2 gpurun_out/pmc_sq.err; [ $rc -eq 0 ] || exit $rc ;;
     pmc)
       for ctr in FETCH_SIZE WRITE_SIZE; do
-        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -d gpurun_out/pmc_$ctr -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --layer-reps 3 > /dev/null 2> gpurun_out/pmc_$ctr.err
+        timeout -k 10 600 rocprofv3 --pmc $ctr --kernel-trace -f csv -d gpurun_out/pmc_$ctr -o run -- python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --layer-reps 3 > /dev/null 2> gpurun_out/pmc_$ctr.err
         rc=$?; echo "pmc $ctr rc=$rc"; tail -2 gpurun_out/pmc_$ctr.err; [ $rc -eq 0 ] || exit $rc
       done ;;
   esac

@@ -148,7 +148,7 @@ bool allow_big_lds(const void *kern) {
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
@@ -159,14 +159,25 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     a.tiles_x = t.tx;
     constexpr int nblk_cols = WN * NW * 16;
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G>;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
-    hipLaunchKernelGGL(kern, grid, dim3(256), t.lds, st, a);
+    // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
+    const size_t epi_lds = (size_t)4 * 16 * (NW * 16 + 4) * 4;
+    hipLaunchKernelGGL(kern, grid, dim3(256), t.lds > epi_lds ? t.lds : epi_lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
 
-// pick the wave tiling from the number of packed output columns
+// pick the wave tiling from the number of packed output columns.
+// CISTA_VARIANT selects the tiling family (A/B builds for scripts/layer_bench.py):
+//   0: MT_W=8 x NW=4 waves, no B prefetch
+//   1: MT_W=16 x NW=2 waves with B-fragment prefetch where the epilogue allows NW=2
+#ifndef CISTA_VARIANT
+#define CISTA_VARIANT 1
+#endif
+#ifndef CISTA_PF_MT
+#define CISTA_PF_MT 12
+#endif
 template <int STAGE, int EPI, int G>
 int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
@@ -176,6 +187,12 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
     } else if constexpr (EPI == EPI_UP_Q) {      // needs WN == 1
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
+        return CISTA_ERR_UNSUPPORTED;
+    } else if constexpr (CISTA_VARIANT == 1 && G <= 2) {
+        constexpr int MT = CISTA_PF_MT;
+        if (a.N % 128 == 0) return launch_conv_cfg<MT, 2, 1, 4, STAGE, EPI, G, true>(a, st);
+        if (a.N == 64) return launch_conv_cfg<MT, 2, 2, 2, STAGE, EPI, G, true>(a, st);
+        if (a.N == 32) return launch_conv_cfg<MT, 2, 4, 1, STAGE, EPI, G, true>(a, st);
         return CISTA_ERR_UNSUPPORTED;
     } else {
         if (a.N >= 256 && a.N % 256 == 0) return launch_conv_cfg<8, 4, 1, 4, STAGE, EPI, G>(a, st);

@@ -94,62 +94,115 @@ __device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &
 // Staging of one 32-channel K-chunk of the halo tile into LDS.
 // LDS image (u32x4 units): [part hi/lo][kgroup 0..3 (8 channels)][HPpad halo pixels]
 // ------------------------------------------------------------------------------------------
+// Thread mapping: item -> (hp = 8*(it>>5) + (it&7), g = (it>>3)&3): each 8-lane ds_write_b128
+// group writes 8 consecutive slots of one k-group plane (bank-conflict free), and the 4 k-group
+// lanes of a pixel read its 128 contiguous bytes.  Loads of BATCH items are issued before any
+// conversion so their latencies overlap.
+template <int STAGE>
+__device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, int ix0, int HWd,
+                                           const float *seg, int segC, int choff, int hp, int g,
+                                           float4 &v0, float4 &v1) {
+    const int hy = hp / HWd;
+    const int hx = hp - hy * HWd;
+    if constexpr (STAGE == STAGE_UP) {
+        // virtual input = ReflectionPad2d(1)(interpolate(h, 2x, bilinear, align_corners=False))
+        const int Hu = 2 * a.Hin, Wu = 2 * a.Win;
+        const int Y = reflect_clamp(iy0 + hy, Hu);
+        const int X = reflect_clamp(ix0 + hx, Wu);
+        float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
+        float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const int y0 = (int)sy, x0 = (int)sx;
+        const int y1 = y0 + (y0 < a.Hin - 1 ? 1 : 0);
+        const int x1 = x0 + (x0 < a.Win - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1;
+        const float lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+        const size_t rowstride = (size_t)a.Win * segC;
+        const float *base = seg + (size_t)b * a.Hin * rowstride + choff + g * 8;
+        const float *p00 = base + (size_t)y0 * rowstride + (size_t)x0 * segC;
+        const float *p01 = base + (size_t)y0 * rowstride + (size_t)x1 * segC;
+        const float *p10 = base + (size_t)y1 * rowstride + (size_t)x0 * segC;
+        const float *p11 = base + (size_t)y1 * rowstride + (size_t)x1 * segC;
+        float r[8];
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+            const float4 a00 = *(const float4 *)(p00 + 4 * h);
+            const float4 a01 = *(const float4 *)(p01 + 4 * h);
+            const float4 a10 = *(const float4 *)(p10 + 4 * h);
+            const float4 a11 = *(const float4 *)(p11 + 4 * h);
+            // torch order: h0l*(w0l*x00 + w1l*x01) + h1l*(w0l*x10 + w1l*x11)
+            r[4 * h + 0] = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
+            r[4 * h + 1] = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
+            r[4 * h + 2] = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
+            r[4 * h + 3] = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
+        }
+        v0 = make_float4(r[0], r[1], r[2], r[3]);
+        v1 = make_float4(r[4], r[5], r[6], r[7]);
+    } else {
+        const int iy = reflect_clamp(iy0 + hy, a.Hin);
+        const int ix = reflect_clamp(ix0 + hx, a.Win);
+        const float *p = seg + (((size_t)b * a.Hin + iy) * a.Win + ix) * segC + choff + g * 8;
+        v0 = *(const float4 *)p;
+        v1 = *(const float4 *)(p + 4);
+    }
+}
+
 template <int STAGE>
 __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
                                             int ix0, int HH, int HWd, int HPpad,
                                             const float *seg, int segC, int choff) {
+    constexpr int BATCH = STAGE == STAGE_UP ? 2 : 4;
     const int HP = HH * HWd;
-    const int nitems = HP * 4;
-    for (int it = threadIdx.x; it < nitems; it += blockDim.x) {
-        const int g = it & 3;
-        const int hp = it >> 2;
-        const int hy = hp / HWd;
-        const int hx = hp - hy * HWd;
-        float4 v0, v1;
-        if constexpr (STAGE == STAGE_UP) {
-            // virtual input = ReflectionPad2d(1)(interpolate(h, 2x, bilinear, align_corners=False))
-            const int Hu = 2 * a.Hin, Wu = 2 * a.Win;
-            const int Y = reflect_clamp(iy0 + hy, Hu);
-            const int X = reflect_clamp(ix0 + hx, Wu);
-            float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
-            float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
-            const int y0 = (int)sy, x0 = (int)sx;
-            const int y1 = y0 + (y0 < a.Hin - 1 ? 1 : 0);
-            const int x1 = x0 + (x0 < a.Win - 1 ? 1 : 0);
-            const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1;
-            const float lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
-            const size_t rowstride = (size_t)a.Win * segC;
-            const float *base = seg + (size_t)b * a.Hin * rowstride + choff + g * 8;
-            const float *p00 = base + (size_t)y0 * rowstride + (size_t)x0 * segC;
-            const float *p01 = base + (size_t)y0 * rowstride + (size_t)x1 * segC;
-            const float *p10 = base + (size_t)y1 * rowstride + (size_t)x0 * segC;
-            const float *p11 = base + (size_t)y1 * rowstride + (size_t)x1 * segC;
-            float r[8];
+    const int nitems = ((HP + 7) & ~7) * 4;
+    for (int it0 = threadIdx.x; it0 < nitems; it0 += BATCH * 256) {
+        float4 v0[BATCH], v1[BATCH];
+        int hps[BATCH], gs[BATCH];
 #pragma unroll
-            for (int h = 0; h < 2; ++h) {
-                const float4 a00 = *(const float4 *)(p00 + 4 * h);
-                const float4 a01 = *(const float4 *)(p01 + 4 * h);
-                const float4 a10 = *(const float4 *)(p10 + 4 * h);
-                const float4 a11 = *(const float4 *)(p11 + 4 * h);
-                // torch order: h0l*(w0l*x00 + w1l*x01) + h1l*(w0l*x10 + w1l*x11)
-                r[4 * h + 0] = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
-                r[4 * h + 1] = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
-                r[4 * h + 2] = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
-                r[4 * h + 3] = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
-            }
-            v0 = make_float4(r[0], r[1], r[2], r[3]);
-            v1 = make_float4(r[4], r[5], r[6], r[7]);
-        } else {
-            const int iy = reflect_clamp(iy0 + hy, a.Hin);
-            const int ix = reflect_clamp(ix0 + hx, a.Win);
-            const float *p = seg + (((size_t)b * a.Hin + iy) * a.Win + ix) * segC + choff + g * 8;
-            v0 = *(const float4 *)p;
-            v1 = *(const float4 *)(p + 4);
+        for (int u = 0; u < BATCH; ++u) {
+            const int it = it0 + u * 256;
+            int hp = ((it >> 5) << 3) | (it & 7);
+            gs[u] = (it >> 3) & 3;
+            hps[u] = (it < nitems && hp < HP) ? hp : -1;
+            hp = hps[u] < 0 ? 0 : hp;
+            stage_load<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, gs[u], v0[u], v1[u]);
         }
-        u32x4 hi, lo;
-        split8(v0, v1, hi, lo);
-        smem[g * HPpad + hp] = hi;
-        smem[(4 + g) * HPpad + hp] = lo;
+#pragma unroll
+        for (int u = 0; u < BATCH; ++u) {
+            if (hps[u] < 0) continue;
+            u32x4 hi, lo;
+            split8(v0[u], v1[u], hi, lo);
+            smem[gs[u] * HPpad + hps[u]] = hi;
+            smem[(4 + gs[u]) * HPpad + hps[u]] = lo;
+        }
+    }
+}
+
+// one tap of one K-chunk: MT_W x NW tiles, 3 split passes each.  Software-pipelined by hand:
+// the A fragments of m-tile m+1 are read while m's MFMAs run, and sched_barrier stops the
+// compiler from hoisting every LDS read of the tap up front (which spills at 256 VGPRs).
+template <int MT_W, int NW>
+__device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *smem,
+                                         const int (&abase)[MT_W], int toff, int HPpad,
+                                         const u32x4 (&bh)[NW], const u32x4 (&bl)[NW]) {
+    u32x4 ah[2], al[2];
+    ah[0] = smem[abase[0] + toff];
+    al[0] = smem[4 * HPpad + abase[0] + toff];
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m) {
+        if (m + 1 < MT_W) {
+            ah[(m + 1) & 1] = smem[abase[m + 1] + toff];
+            al[(m + 1) & 1] = smem[4 * HPpad + abase[m + 1] + toff];
+        }
+        const f16x8 xh = __builtin_bit_cast(f16x8, ah[m & 1]);
+        const f16x8 xl = __builtin_bit_cast(f16x8, al[m & 1]);
+#pragma unroll
+        for (int n = 0; n < NW; ++n) {
+            const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
+            const f16x8 wl = __builtin_bit_cast(f16x8, bl[n]);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wl, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wh, acc[m][n], 0, 0, 0);
+        }
+        __builtin_amdgcn_sched_barrier(0);
     }
 }
 
@@ -157,7 +210,7 @@ __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int 
 // The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
 // MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
 // ------------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF>
 __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     static_assert(WM * WN == 4, "4 waves per workgroup");
     static_assert(NW % G == 0, "a wave must hold whole gate groups");
@@ -218,28 +271,48 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         __syncthreads();
 
         const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
-#pragma unroll 1
-        for (int tap = 0; tap < 9; ++tap) {
+        if constexpr (PF) {
+            // opaque to LICM: otherwise all 9 x MT_W tap addresses are hoisted out of the K loop
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) asm volatile("" : "+v"(abase[m]));
+            // B fragments of tap t+1 are loaded while tap t's MFMAs run (L2 latency hidden)
             u32x4 bh[NW], bl[NW];
-            const u32x4 *wq = wp + (size_t)tap * tapstride;
 #pragma unroll
             for (int n = 0; n < NW; ++n) {
-                bh[n] = wq[n * 128];
-                bl[n] = wq[n * 128 + 64];
+                bh[n] = wp[n * 128];
+                bl[n] = wp[n * 128 + 64];
             }
-            const int toff = (tap / 3) * HWd + (tap % 3);
 #pragma unroll
-            for (int m = 0; m < MT_W; ++m) {
-                const f16x8 ah = __builtin_bit_cast(f16x8, smem[abase[m] + toff]);
-                const f16x8 al = __builtin_bit_cast(f16x8, smem[4 * HPpad + abase[m] + toff]);
+            for (int tap = 0; tap < 9; ++tap) {
+                u32x4 nh[NW], nl[NW];
+                if (tap < 8) {
+                    const u32x4 *wq = wp + (size_t)(tap + 1) * tapstride;
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        nh[n] = wq[n * 128];
+                        nl[n] = wq[n * 128 + 64];
+                    }
+                }
+                mfma_tap<MT_W, NW>(acc, smem, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
+                if (tap < 8) {
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        bh[n] = nh[n];
+                        bl[n] = nl[n];
+                    }
+                }
+            }
+        } else {
+#pragma unroll 1
+            for (int tap = 0; tap < 9; ++tap) {
+                u32x4 bh[NW], bl[NW];
+                const u32x4 *wq = wp + (size_t)tap * tapstride;
 #pragma unroll
                 for (int n = 0; n < NW; ++n) {
-                    const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
-                    const f16x8 wl = __builtin_bit_cast(f16x8, bl[n]);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wh, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, wl, acc[m][n], 0, 0, 0);
-                    acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, wh, acc[m][n], 0, 0, 0);
+                    bh[n] = wq[n * 128];
+                    bl[n] = wq[n * 128 + 64];
                 }
+                mfma_tap<MT_W, NW>(acc, smem, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
             }
         }
     }
@@ -303,62 +376,99 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         return;
     }
 
+    // Epilogue through a per-wave LDS transpose: each m-tile's 16 pixels x (NW*16) columns are
+    // written to LDS as [pixel][column] and read back so that a lane owns 4 consecutive
+    // channels of one pixel -> the aux reads and output writes are 16-byte, fully coalesced
+    // (16 lanes = one pixel's 256-byte channel run) instead of 4-byte scattered accesses.
+    __syncthreads();                                       // staging LDS is free from here on
+    constexpr int LDT = NW * 16 + 4;                       // padded row: conflict-free writes
+    constexpr int CG = (NW / G) * 4;                       // 4-channel groups per pixel
+    float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
+    const int grp = lane >> 4;
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
-            if (p >= npix) continue;
-            const int py = p / a.TW;
-            const int px = p - py * a.TW;
-            const int oy = oy0 + py, ox = ox0 + px;
-            if (oy >= a.Hout || ox >= a.Wout) continue;
-            const size_t pix = ((size_t)b * a.Hout + oy) * a.Wout + ox;
-            if constexpr (G == 1) {
+        for (int n = 0; n < NW; ++n)
 #pragma unroll
-                for (int n = 0; n < NW; ++n) {
-                    const int ch = (nt0 + n) * 16 + col;
-                    float v = acc[m][n][j] + a.bias[ch];
-                    const size_t o = pix * a.Cout + ch;
-                    if constexpr (EPI == EPI_RELU) {
-                        v = fmaxf(v, 0.0f);
-                    } else if constexpr (EPI == EPI_ISTA_D) {
-                        v = a.aux0[o] - v;
-                    } else if constexpr (EPI == EPI_ISTA_P) {
-                        const float x = v + a.aux0[o];
-                        const float lam = a.lambda[ch];
-                        v = fmaxf(x - lam, 0.0f) - fmaxf(-x - lam, 0.0f);
-                    } else if constexpr (EPI == EPI_LSTC_OUT) {
-                        v = sigmoidf_(v) * tanhf(a.aux0[o]);
+            for (int j = 0; j < 4; ++j) T[(4 * grp + j) * LDT + n * 16 + col] = acc[m][n][j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+        for (int it0 = 0; it0 < 16 * CG; it0 += 64) {
+            const int it = it0 + lane;
+            if (it < 16 * CG) {
+                const int row = it / CG, cg = it - row * CG;
+                const int q = cg >> 2, c4 = (cg & 3) * 4;
+                const int p = (wm * MT_W + m) * 16 + row;
+                const int py = p / a.TW;
+                const int px = p - py * a.TW;
+                const int oy = oy0 + py, ox = ox0 + px;
+                if (p < npix && oy < a.Hout && ox < a.Wout) {
+                    const size_t pix = ((size_t)b * a.Hout + oy) * a.Wout + ox;
+                    float4 v[G];
+#pragma unroll
+                    for (int g = 0; g < G; ++g) {
+                        const int nl = q * G + g;                      // n-tile within the wave
+                        const float *src = T + row * LDT + nl * 16 + c4;
+                        const float4 bb = *(const float4 *)(a.bias + (nt0 + nl) * 16 + c4);
+                        v[g] = make_float4(src[0] + bb.x, src[1] + bb.y, src[2] + bb.z, src[3] + bb.w);
                     }
-                    a.out0[o] = v;
-                }
-            } else {
-#pragma unroll
-                for (int q = 0; q < NW / G; ++q) {
-                    const int cblk = (nt0 / G) + q;
-                    const int ch = cblk * 16 + col;           // channel within one gate
+                    const int ch = ((nt0 / G) + q) * 16 + c4;          // channel within a gate
                     const size_t o = pix * a.Cout + ch;
-                    if constexpr (EPI == EPI_LSTC_CELL) {
+                    float r[4], r1[4];
+                    const float *vv = reinterpret_cast<const float *>(v);
+                    if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? fmaxf(vv[e], 0.0f) : vv[e];
+                    } else if constexpr (EPI == EPI_ISTA_D) {
+                        const float4 x1 = *(const float4 *)(a.aux0 + o);
+                        const float *xx = reinterpret_cast<const float *>(&x1);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
+                    } else if constexpr (EPI == EPI_ISTA_P) {
+                        const float4 z = *(const float4 *)(a.aux0 + o);
+                        const float4 lm = *(const float4 *)(a.lambda + ch);
+                        const float *zz = reinterpret_cast<const float *>(&z);
+                        const float *ll = reinterpret_cast<const float *>(&lm);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float x = vv[e] + zz[e];
+                            r[e] = fmaxf(x - ll[e], 0.0f) - fmaxf(-x - ll[e], 0.0f);
+                        }
+                    } else if constexpr (EPI == EPI_LSTC_OUT) {
+                        const float4 c = *(const float4 *)(a.aux0 + o);
+                        const float *cc = reinterpret_cast<const float *>(&c);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) r[e] = sigmoidf_(vv[e]) * tanhf(cc[e]);
+                    } else if constexpr (EPI == EPI_LSTC_CELL) {
                         // packed n-tile order per channel block: (in, forget)
-                        const float gi = sigmoidf_(acc[m][q * 2 + 0][j] + a.bias[(nt0 + q * 2 + 0) * 16 + col]);
-                        const float gf = sigmoidf_(acc[m][q * 2 + 1][j] + a.bias[(nt0 + q * 2 + 1) * 16 + col]);
-                        const float cp = a.aux0 ? a.aux0[o] : 0.0f;
-                        a.out0[o] = gf * cp + gi * a.aux1[o];
+                        const float4 z0 = *(const float4 *)(a.aux1 + o);
+                        const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float *zz = reinterpret_cast<const float *>(&z0);
+                        const float *pp = reinterpret_cast<const float *>(&cp);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e)
+                            r[e] = sigmoidf_(vv[4 + e]) * pp[e] + sigmoidf_(vv[e]) * zz[e];
                     } else if constexpr (EPI == EPI_LSTM) {
                         // packed n-tile order per channel block: (in, remember, out, cell)
-                        const float gi = sigmoidf_(acc[m][q * 4 + 0][j] + a.bias[(nt0 + q * 4 + 0) * 16 + col]);
-                        const float gr = sigmoidf_(acc[m][q * 4 + 1][j] + a.bias[(nt0 + q * 4 + 1) * 16 + col]);
-                        const float go = sigmoidf_(acc[m][q * 4 + 2][j] + a.bias[(nt0 + q * 4 + 2) * 16 + col]);
-                        const float gc = tanhf(acc[m][q * 4 + 3][j] + a.bias[(nt0 + q * 4 + 3) * 16 + col]);
-                        const float cp = a.aux0 ? a.aux0[o] : 0.0f;
-                        const float c = gr * cp + gi * gc;
-                        a.out0[o] = go * tanhf(c);
-                        a.out1[o] = c;
+                        const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float *pp = reinterpret_cast<const float *>(&cp);
+#pragma unroll
+                        for (int e = 0; e < 4; ++e) {
+                            const float c = sigmoidf_(vv[4 + e]) * pp[e] + sigmoidf_(vv[e]) * tanhf(vv[12 + e]);
+                            r1[e] = c;
+                            r[e] = sigmoidf_(vv[8 + e]) * tanhf(c);
+                        }
+                        *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     }
+                    *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
                 }
             }
         }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
 }
 
