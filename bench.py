@@ -198,17 +198,14 @@ def cpu_baseline(torch, model, vox, H, W, n_frames):
 
 def main():
     args = parse()
-    rank = int(os.environ.get("RANK", 0))
-    world = int(os.environ.get("WORLD_SIZE", 1))
-    local_rank = int(os.environ.get("LOCAL_RANK", 0))
     import torch
-    import torch.distributed as dist
     from v2e2v_amd import CistaLSTCNet, _lib
+    from v2e2v_amd import dist as vd
 
+    rank, world, local_rank = vd.env_rank()
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
-    if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+    vd.init("nccl", device)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
 
     model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
@@ -222,20 +219,15 @@ def main():
         for _ in range(args.warmup):
             run_sequence(torch, model, vox, B, H, W, device)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        vd.barrier()
         t0 = time.perf_counter()
         for _ in range(args.steps):
             rec, _ = run_sequence(torch, model, vox, B, H, W, device)
         torch.cuda.synchronize()
-        if world > 1:
-            dist.barrier()
+        vd.barrier()
         elapsed = time.perf_counter() - t0
     finite = bool(torch.isfinite(rec).all())
-    t = torch.tensor([elapsed], device=device, dtype=torch.float64)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t.item())
+    elapsed = vd.max_over_ranks(elapsed, device)
     frames = world * B * L * args.steps
     value = frames / elapsed
 
@@ -249,6 +241,19 @@ def main():
                     flop_per_launch=2 * dom["macs"],
                     note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean "
                          "duration; peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+
+    # HBM bytes per launch of the same kernel from the committed PMC passes (FETCH_SIZE and
+    # WRITE_SIZE, separate rocprofv3 runs, gfx950 read correction): scripts/pmc_traffic.py
+    import glob
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    if tfiles:
+        try:
+            tl = json.load(open(tfiles[-1]))["layers"].get(dom_name)
+            if tl:
+                roofline["traffic"] = tl["hbm_bytes_per_launch"]
+                roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
+        except (OSError, ValueError, KeyError):
+            pass
 
     cpu = None
     psnr_vs_ref = rel_vs_ref = None
@@ -289,7 +294,7 @@ def main():
         }
         print(json.dumps(out), flush=True)
     if world > 1:
-        dist.destroy_process_group()
+        torch.distributed.destroy_process_group()
 
 
 if __name__ == "__main__":

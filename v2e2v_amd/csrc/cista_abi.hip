@@ -111,16 +111,25 @@ size_t lds_bytes(int TH, int TW, int S) {
     return (size_t)((HP + 15) & ~15) * 8 * 16;
 }
 
-Tile choose_tile(int Hout, int Wout, int block_px, int S) {
+// max_items: staging items (HP rounded to 8, x4 k-groups) one workgroup may hold in registers
+// (0 = unlimited); nbuf: LDS images (2 for the double-buffered loop)
+Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf) {
     Tile best{1, 1, Hout, Wout, 0};
     double best_eff = -1.0;
     size_t best_lds = ~(size_t)0;
     const size_t lds_cap = 80 * 1024;   // two workgroups per CU
     for (int TW = 1; TW <= block_px && TW <= Wout; ++TW) {
+#if CISTA_TW16
+        // 16-pixel m-tiles that never wrap a tile row read LDS without bank conflicts
+        if (Wout >= 16 && (TW % 16) != 0) continue;
+#endif
         int TH = block_px / TW;
         if (TH > Hout) TH = Hout;
         if (TH < 1) continue;
-        const size_t lds = lds_bytes(TH, TW, S);
+        auto items = [&](int th) { return ((((th - 1) * S + 3) * ((TW - 1) * S + 3) + 7) & ~7) * 4; };
+        while (max_items && TH > 1 && items(TH) > max_items) --TH;
+        if (max_items && items(TH) > max_items) continue;
+        const size_t lds = lds_bytes(TH, TW, S) * nbuf;
         if (lds > lds_cap) continue;
         const int ty = (Hout + TH - 1) / TH, tx = (Wout + TW - 1) / TW;
         const double eff = (double)Hout * Wout / ((double)ty * tx * block_px);
@@ -148,18 +157,18 @@ bool allow_big_lds(const void *kern) {
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
-    const Tile t = choose_tile(a.Hout, a.Wout, block_px, S);
+    const Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1);
     a.TH = t.TH;
     a.TW = t.TW;
     a.tiles_y = t.ty;
     a.tiles_x = t.tx;
     constexpr int nblk_cols = WN * NW * 16;
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF>;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
     // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
@@ -172,8 +181,12 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 // CISTA_VARIANT selects the tiling family (A/B builds for scripts/layer_bench.py):
 //   0: MT_W=8 x NW=4 waves, no B prefetch
 //   1: MT_W=16 x NW=2 waves with B-fragment prefetch where the epilogue allows NW=2
+//   2: double-buffered K loop (next halo chunk prefetched into registers), B prefetch
 #ifndef CISTA_VARIANT
-#define CISTA_VARIANT 1
+#define CISTA_VARIANT 2
+#endif
+#ifndef CISTA_TW16
+#define CISTA_TW16 0
 #endif
 #ifndef CISTA_PF_MT
 #define CISTA_PF_MT 12
@@ -188,7 +201,17 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (CISTA_VARIANT == 1 && G <= 2) {
+    } else if constexpr (CISTA_VARIANT == 2 && STAGE == STAGE_S1) {
+        // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
+        if constexpr (G == 4) {
+            if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
+        } else {
+            if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N == 64) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N == 32) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);
+        }
+        return CISTA_ERR_UNSUPPORTED;
+    } else if constexpr (CISTA_VARIANT >= 1 && G <= 2) {
         constexpr int MT = CISTA_PF_MT;
         if (a.N % 128 == 0) return launch_conv_cfg<MT, 2, 1, 4, STAGE, EPI, G, true>(a, st);
         if (a.N == 64) return launch_conv_cfg<MT, 2, 2, 2, STAGE, EPI, G, true>(a, st);

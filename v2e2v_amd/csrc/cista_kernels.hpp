@@ -176,6 +176,41 @@ __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int 
     }
 }
 
+// Split staging for the double-buffered K loop: issue the global loads of the NEXT chunk into
+// registers before the current chunk's MFMAs, convert + write them to the other LDS buffer
+// after.  The host guarantees (HP rounded to 8) * 4 <= NI * blockDim.x items.
+template <int STAGE, int NI>
+__device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, int ix0, int HH,
+                                            int HWd, const float *seg, int segC, int choff,
+                                            float4 (&v0)[NI], float4 (&v1)[NI], int (&hps)[NI],
+                                            int (&gs)[NI]) {
+    const int HP = HH * HWd;
+    const int nitems = ((HP + 7) & ~7) * 4;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const int it = threadIdx.x + u * 256;
+        int hp = ((it >> 5) << 3) | (it & 7);
+        gs[u] = (it >> 3) & 3;
+        hps[u] = (it < nitems && hp < HP) ? hp : -1;
+        hp = hps[u] < 0 ? 0 : hp;
+        stage_load<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, gs[u], v0[u], v1[u]);
+    }
+}
+
+template <int NI>
+__device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4 (&v0)[NI],
+                                             const float4 (&v1)[NI], const int (&hps)[NI],
+                                             const int (&gs)[NI]) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        if (hps[u] < 0) continue;
+        u32x4 hi, lo;
+        split8(v0[u], v1[u], hi, lo);
+        buf[gs[u] * HPpad + hps[u]] = hi;
+        buf[(4 + gs[u]) * HPpad + hps[u]] = lo;
+    }
+}
+
 // one tap of one K-chunk: MT_W x NW tiles, 3 split passes each.  Software-pipelined by hand:
 // the A fragments of m-tile m+1 are read while m's MFMAs run, and sched_barrier stops the
 // compiler from hoisting every LDS read of the tap up front (which spills at 256 VGPRs).
@@ -210,8 +245,9 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
 // The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
 // MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
 // ------------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0>
 __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
+    // NI > 0: double-buffered K loop (two LDS images, next chunk's loads in NI x 8 VGPRs)
     static_assert(WM * WN == 4, "4 waves per workgroup");
     static_assert(NW % G == 0, "a wave must hold whole gate groups");
     extern __shared__ u32x4 smem[];
@@ -262,10 +298,67 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     const int nchunks = kc0 + (a.in1 ? (a.c1 >> 5) : 0);
     const size_t tapstride = (size_t)NT * 2 * 64;   // u32x4 per tap
 
+    auto seg_of = [&](int kc, const float *&seg, int &segC, int &choff) {
+        seg = kc < kc0 ? a.in0 : a.in1;
+        segC = kc < kc0 ? a.c0 : a.c1;
+        choff = (kc < kc0 ? kc : kc - kc0) * 32;
+    };
+    if constexpr (NI > 0) {
+        static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
+        {
+            const float *seg; int segC, choff;
+            seg_of(0, seg, segC, choff);
+            stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff);
+        }
+        __syncthreads();
+        for (int kc = 0; kc < nchunks; ++kc) {
+            const u32x4 *cur = smem + (kc & 1) * 8 * HPpad;
+            u32x4 *nxt = smem + ((kc + 1) & 1) * 8 * HPpad;
+            const bool more = kc + 1 < nchunks;
+            const float *nseg; int nsegC, nchoff;
+            seg_of(more ? kc + 1 : kc, nseg, nsegC, nchoff);
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) asm volatile("" : "+v"(abase[m]));
+            const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
+            u32x4 bh[NW], bl[NW];
+#pragma unroll
+            for (int n = 0; n < NW; ++n) {
+                bh[n] = wp[n * 128];
+                bl[n] = wp[n * 128 + 64];
+            }
+            float4 sv0[NI], sv1[NI];
+            int shp[NI], sg[NI];
+#pragma unroll
+            for (int tap = 0; tap < 9; ++tap) {
+                u32x4 nh[NW], nl[NW];
+                if (tap < 8) {
+                    const u32x4 *wq = wp + (size_t)(tap + 1) * tapstride;
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        nh[n] = wq[n * 128];
+                        nl[n] = wq[n * 128 + 64];
+                    }
+                }
+                // the next chunk's halo loads go out after B(0), B(1): the waits for those two
+                // do not include them (vmcnt is in order); they land under taps 0..1
+                if (tap == 0 && more)
+                    stage_issue<STAGE, NI>(a, b, iy0, ix0, HH, HWd, nseg, nsegC, nchoff, sv0, sv1, shp, sg);
+                mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
+                if (tap < 8) {
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        bh[n] = nh[n];
+                        bl[n] = nl[n];
+                    }
+                }
+            }
+            if (more) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg);
+            __syncthreads();
+        }
+    } else
     for (int kc = 0; kc < nchunks; ++kc) {
-        const float *seg = kc < kc0 ? a.in0 : a.in1;
-        const int segC = kc < kc0 ? a.c0 : a.c1;
-        const int choff = (kc < kc0 ? kc : kc - kc0) * 32;
+        const float *seg; int segC, choff;
+        seg_of(kc, seg, segC, choff);
         __syncthreads();
         stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff);
         __syncthreads();

@@ -1,0 +1,58 @@
+"""Multi-GPU plumbing: one process per GPU (torchrun), sequences sharded across ranks.
+
+Inference has no exchange step -- sequences are independent (no BN/IN), so each
+rank reconstructs its own shard and nothing crosses xGMI on the data path.  The only
+collectives are the benchmark's barrier and max-over-ranks timing (RCCL, or gloo on CPU for the
+tests).  DDP for BPTT training (one gradient all-reduce per step) arrives with the backward.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+def env_rank():
+    """(rank, world_size, local_rank) from the torchrun environment (defaults: single process)."""
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("WORLD_SIZE", 1)),
+            int(os.environ.get("LOCAL_RANK", 0)))
+
+
+def init(backend: str | None = None, device: torch.device | None = None):
+    """Initialise the default process group when WORLD_SIZE > 1 (MASTER_ADDR=127.0.0.1)."""
+    rank, world, local = env_rank()
+    if world > 1 and not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
+        kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
+        dist.init_process_group(backend, rank=rank, world_size=world, **kw)
+    return rank, world, local
+
+
+def shard(n_items: int, rank: int, world: int) -> range:
+    """Contiguous, balanced partition of n_items sequences; every item on exactly one rank."""
+    base, extra = divmod(n_items, world)
+    start = rank * base + min(rank, extra)
+    return range(start, start + base + (1 if rank < extra else 0))
+
+
+def max_over_ranks(x: float, device=None) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(x: float, device=None) -> float:
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size() == 1:
+        return float(x)
+    t = torch.tensor([float(x)], dtype=torch.float64, device=device)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+def barrier():
+    if dist.is_available() and dist.is_initialized():
+        dist.barrier()
