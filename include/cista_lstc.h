@@ -158,6 +158,44 @@ int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, i
                        int W, const cista_frame_io *io, void *workspace, size_t workspace_bytes,
                        void *stream);
 
+/* ---- training: BPTT backward (reference train_e2v.py:108-130
+ * differentiates through the whole recurrent sequence with autograd) ----
+ * A training frame runs cista_forward_train, which also fills a `saved` buffer with the
+ * activations the backward needs; cista_backward then takes the gradients of the frame's five
+ * outputs and returns the gradients of its inputs (previous image and states: BPTT) and of
+ * all 25 parameters.  Both require base_channels in {32, 64}. */
+size_t cista_saved_bytes(const cista_config *cfg, int B, int H, int W);
+size_t cista_train_workspace_bytes(const cista_config *cfg, int B, int H, int W);
+int cista_forward_train(const cista_config *cfg, const void *packed, int B, int H, int W,
+                        const cista_frame_io *io, void *saved, size_t saved_bytes,
+                        void *workspace, size_t workspace_bytes, void *stream);
+
+typedef struct {
+    const float *g_rec;        /* dL/d rec      (B,1,H,W)       NULL = 0            */
+    const float *g_c_lstc;     /* dL/d states[0] NHWC (B,h,w,2C) NULL = 0           */
+    const float *g_z;          /* dL/d states[1] NHWC (B,h,w,2C) NULL = 0           */
+    const float *g_h;          /* dL/d states[2][0] (B,h,w,C)    NULL = 0           */
+    const float *g_c;          /* dL/d states[2][1] (B,h,w,C)    NULL = 0           */
+    float *g_prev_image;       /* out (B,1,H,W); NULL = not needed                  */
+    float *g_c_lstc_prev;      /* out (B,h,w,2C); NULL = not needed / prev was None */
+    float *g_z_prev;           /* out (B,h,w,2C)                                    */
+    float *g_h_prev;           /* out (B,h,w,C)                                     */
+    float *g_c_prev;           /* out (B,h,w,C)                                     */
+} cista_grad_io;
+
+/* parameter gradients, same fields / layouts as cista_params; written (not accumulated) */
+typedef struct {
+    float *We_w, *We_b, *Wi_w, *Wi_b, *W0_w, *W0_b;
+    float *gates_w, *gates_b, *out_gates_w, *out_gates_b, *P0_w, *P0_b;
+    float *lambda, *D_w, *D_b, *P_w, *P_b;
+    float *Dg_w, *Dg_b, *lstm_w, *lstm_b, *up_w, *up_b, *final_w, *final_b;
+} cista_param_grads;
+
+int cista_backward(const cista_config *cfg, const void *packed, const cista_params *params,
+                   int B, int H, int W, const cista_frame_io *io, const void *saved,
+                   size_t saved_bytes, const cista_grad_io *grads, const cista_param_grads *pgrads,
+                   void *workspace, size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,114 @@
+"""BPTT backward of the HIP path against gradients produced by the
+real reference's autograd on CPU (tests/golden/make_golden_grads.py).
+
+Bar: max|hip - ref| / max|ref| <= 1e-3 per gradient tensor.  The reference's own fp32 gradients
+differ from its fp64 gradients by up to 5e-5 on these fixtures (stored as *_noise32_*), so the
+bar is 20x the reference's fp32 noise; the forward outputs keep the 1e-4 bar.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fixtures as fx
+from tests.conftest import rel_err
+from v2e2v_amd import CistaLSTCNet
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+GTOL = 1e-3
+
+
+def model(C=64, depth=5):
+    m = CistaLSTCNet([32, 48], base_channels=C, depth=depth, num_bins=5)
+    params = fx.stress_params(C, depth, 5, seed=21, lam=0.05)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, depth)
+    m.load_state_dict(sd, strict=True)
+    return m.to(DEV)
+
+
+def grads_by_name(m):
+    out = {}
+    for k, p in m.named_parameters():
+        out[k.replace("lista_blocks.0.", "lista.")] = p.grad.detach().cpu().numpy()
+    return out
+
+
+def gpu(x, rg=False):
+    return torch.from_numpy(np.ascontiguousarray(x)).to(DEV).requires_grad_(rg)
+
+
+def test_one_frame_all_gradients(golden):
+    d = golden("grads_32x48.npz")
+    m = model()
+    leaves = [gpu(d["g1_prev_image"], True)] + [gpu(d[f"g1_prev_{n}"], True) for n in ("c_lstc", "z", "h", "c")]
+    rec, st = m(gpu(d["voxels"][1]), leaves[0], [leaves[1], leaves[2], (leaves[3], leaves[4])])
+    outs = [rec, st[0], st[1], st[2][0], st[2][1]]
+    loss = sum((o * gpu(d[f"g1_R{i}"])).sum() for i, o in enumerate(outs))
+    loss.backward()
+    torch.cuda.synchronize()
+    bad = {}
+    for k, g in grads_by_name(m).items():
+        e = rel_err(g, d[f"g1_f32_param_{k}"])
+        if not e < GTOL:
+            bad[k] = e
+    for i, n in enumerate(["prev_image", "c_lstc", "z", "h", "c"]):
+        e = rel_err(leaves[i].grad.detach().cpu().numpy(), d[f"g1_f32_grad_{n}"])
+        if not e < GTOL:
+            bad["input:" + n] = e
+    assert not bad, bad
+
+
+def test_three_frame_bptt_l1(golden):
+    """train_e2v.py:108-120: prev_img = output.clone() (no detach), states carried, L1 loss on
+    the last frame, one backward through all frames."""
+    d = golden("grads_32x48.npz")
+    m = model()
+    B, _, H, W = d["g2_target"].shape
+    prev = torch.zeros(B, 1, H, W, device=DEV)
+    state = None
+    for s in range(3):
+        out, state = m(gpu(d["voxels"][s]), prev, state)
+        prev = out.clone()
+    loss = torch.nn.functional.l1_loss(out, gpu(d["g2_target"]))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert abs(loss.item() - float(d["g2_f32_loss"])) <= 1e-4 * abs(float(d["g2_f32_loss"]))
+    bad = {}
+    for k, g in grads_by_name(m).items():
+        e = rel_err(g, d[f"g2_f32_param_{k}"])
+        if not e < GTOL:
+            bad[k] = e
+    assert not bad, bad
+
+
+def test_training_forward_equals_inference_forward(golden):
+    d = golden("grads_32x48.npz")
+    m = model()
+    ev = gpu(d["voxels"][0])
+    prev = torch.zeros(2, 1, 32, 48, device=DEV)
+    with torch.no_grad():
+        r0, s0 = m(ev, prev, None)
+    r1, s1 = m(ev, prev, None)                      # grad mode: the training kernels
+    assert r1.requires_grad
+    assert torch.equal(r0, r1.detach())
+    for a, b in zip([s0[0], s0[1], s0[2][0], s0[2][1]], [s1[0], s1[1], s1[2][0], s1[2][1]]):
+        assert torch.equal(a, b.detach())
+
+
+def test_report_gradient_errors(golden, capsys):
+    """Not a bar: prints the measured gradient errors next to the reference's own fp32 noise."""
+    d = golden("grads_32x48.npz")
+    m = model()
+    B, _, H, W = d["g2_target"].shape
+    prev = torch.zeros(B, 1, H, W, device=DEV)
+    state = None
+    for s in range(3):
+        out, state = m(gpu(d["voxels"][s]), prev, state)
+        prev = out.clone()
+    torch.nn.functional.l1_loss(out, gpu(d["g2_target"])).backward()
+    rows = [(k, rel_err(g, d[f"g2_f32_param_{k}"]), float(d[f"g2_noise32_param_{k}"]))
+            for k, g in grads_by_name(m).items()]
+    with capsys.disabled():
+        for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]:
+            print(f"\n  grad {k:40s} hip-vs-ref32 {e:.2e}   ref32-vs-ref64 {n:.2e}", end="")
+        print()

@@ -74,7 +74,8 @@ def test_cpu_tensors_raise_no_fallback():
         m(torch.zeros(1, 5, 32, 32), torch.zeros(1, 1, 32, 32), None)
 
 
-def test_grad_mode_without_backward_raises():
+def test_grad_mode_cpu_raises_no_fallback():
+    """The training path (autograd + HIP backward) is GPU-only as well."""
     m = CistaLSTCNet([32, 32], base_channels=32, depth=1, num_bins=5)
-    with pytest.raises(RuntimeError, match="backward"):
+    with pytest.raises(RuntimeError, match="ROCm"):
         m(torch.zeros(1, 5, 32, 32), torch.zeros(1, 1, 32, 32), None)

@@ -45,6 +45,16 @@ class CistaFrameIO(ctypes.Structure):
 LAYERS = ["input", "W0", "P0", "gates", "out_gates", "ista_D", "ista_P", "Dg", "lstm",
           "upsample", "final"]          # CISTA_LAYER_* ids, in frame order
 
+class CistaGradIO(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in (
+        "g_rec", "g_c_lstc", "g_z", "g_h", "g_c",
+        "g_prev_image", "g_c_lstc_prev", "g_z_prev", "g_h_prev", "g_c_prev")]
+
+
+class CistaParamGrads(ctypes.Structure):
+    _fields_ = [(n, c_void_p) for n in PARAM_FIELDS]
+
+
 STATUS = {0: "ok", 1: "invalid argument", 2: "unsupported configuration", 3: "HIP runtime error",
           4: "workspace too small", 5: "output aliases input"}
 
@@ -80,6 +90,13 @@ def _declare(lib):
         "cista_stage_output": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_void_p,
                                        c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
         "cista_layer_macs": (ctypes.c_double, [P(CistaConfig), c_int, c_int, c_int, c_int]),
+        "cista_saved_bytes": (c_size_t, [P(CistaConfig), c_int, c_int, c_int]),
+        "cista_train_workspace_bytes": (c_size_t, [P(CistaConfig), c_int, c_int, c_int]),
+        "cista_forward_train": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO),
+                                        c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
+        "cista_backward": (c_int, [P(CistaConfig), c_void_p, P(CistaParams), c_int, c_int, c_int,
+                                   P(CistaFrameIO), c_void_p, c_size_t, P(CistaGradIO),
+                                   P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
     }

@@ -7,6 +7,7 @@
 
 #include "../../include/cista_lstc.h"
 #include "cista_kernels.hpp"
+#include "cista_backward.hpp"
 
 using namespace cista;
 
@@ -38,6 +39,7 @@ ConvShape conv_shape(int id, int C) {
 
 struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
+    size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
     size_t wE, wI, bIn, wF, bF, lambda;
     size_t total;
 };
@@ -54,6 +56,13 @@ Layout make_layout(const cista_config &cfg) {
         off = align_up(off + (size_t)s.cout * 4);
         L.sc[i] = off;
         off = align_up(off + 8);
+    }
+    for (int i = 0; i < CV_COUNT; ++i) {
+        const ConvShape s = conv_shape(i, C);
+        L.dwp[i] = off;
+        off = align_up(off + (size_t)(s.cout / 32) * 9 * (s.cin / 16) * 2 * 64 * 16);
+        L.dbp[i] = off;
+        off = align_up(off + (size_t)s.cin * 4);
     }
     L.wE = off; off = align_up(off + (size_t)nb * 9 * (C / 2) * 4);
     L.wI = off; off = align_up(off + (size_t)9 * (C / 2) * 4);
@@ -201,13 +210,13 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (CISTA_VARIANT == 2 && STAGE == STAGE_S1) {
+    } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2)) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
         if constexpr (G == 4) {
             if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
         } else {
             if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4>(a, st);
-            if (a.N == 64) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4>(a, st);
             if (a.N == 32) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);
         }
         return CISTA_ERR_UNSUPPORTED;
@@ -272,13 +281,23 @@ struct Frame {
     float *z;       // LSTC output, then ISTA iterate (in place)       (B,h,w,2C)
     float *hs, *cs; // ConvLSTM state                                  (B,h,w,C)
     float *rec, *pre;
+    // training forward: activations saved for the backward (all NULL at inference)
+    float *gi, *gf, *go;   // ConvLSTC gates (sigmoid)                    (B,h,w,2C) each
+    float *zl;             // ConvLSTC output = ISTA z_0                  (B,h,w,2C)
+    float *v;              // depth x pre-softshrink ISTA values          (B,h,w,2C)
+    float *xs;             // depth x ISTA x_k = x1 - D(z_k)              (B,h,w,C)
+    float *y;              // relu(Dg.conv(z))                            (B,h,w,C)
+    float *lg;             // ConvLSTM gates (i, r, o, g) post-activation (B,h,w,4C)
+    float *u;              // relu(upsamp_conv(...))                      (B,H,W,C)
     hipStream_t st;
 };
 
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
 
-int run_layer(const Frame &f, int layer) {
+int run_layer(const Frame &f, int layer, int it = 0) {
+    const size_t hw = (size_t)f.B * f.h * f.w;
+    const bool zl_in = f.zl && it == 0 && f.cfg->depth > 0;   // ISTA iteration 0 reads z_0
     const int C = f.C, B = f.B, h = f.h, w = f.w;
     ConvArgs a;
     switch (layer) {
@@ -318,32 +337,36 @@ int run_layer(const Frame &f, int layer) {
         case CISTA_LAYER_GATES:     // c = sig(f) c_prev + sig(i) z0, gates(cat(x1, z_prev)) :57-67
             a = conv_args(f.packed, f.L, CV_GATES, C, B, h, w, h, w, f.x1, C, f.z_prev, 2 * C);
             a.out0 = f.c_lstc; a.aux0 = f.c_lstc_prev; a.aux1 = f.z0;
+            a.out1 = f.gi; a.out2 = f.gf;
             return launch_conv<STAGE_S1, EPI_LSTC_CELL, 2>(a, f.st);
         case CISTA_LAYER_OUT_GATES: // z = sig(out_gates(cat(z0, z_prev))) tanh(c)          :63,69
             a = conv_args(f.packed, f.L, CV_OUTG, C, B, h, w, h, w, f.z0, 2 * C, f.z_prev, 2 * C);
-            a.out0 = f.z; a.aux0 = f.c_lstc;
+            a.out0 = (f.zl && f.cfg->depth > 0) ? f.zl : f.z; a.aux0 = f.c_lstc; a.out1 = f.go;
             return launch_conv<STAGE_S1, EPI_LSTC_OUT, 1>(a, f.st);
         case CISTA_LAYER_ISTA_D:    // x = x1 - D(z)                              e2v_model.py:73-74
-            a = conv_args(f.packed, f.L, CV_D, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
-            a.out0 = f.xb; a.aux0 = f.x1;
+            a = conv_args(f.packed, f.L, CV_D, C, B, h, w, h, w, zl_in ? f.zl : f.z, 2 * C, nullptr, 0);
+            a.out0 = f.xs ? f.xs + it * hw * C : f.xb; a.aux0 = f.x1;
             return launch_conv<STAGE_S1, EPI_ISTA_D, 1>(a, f.st);
         case CISTA_LAYER_ISTA_P:    // z = softshrink(P(x) + z, lambda)            :75-77
-            a = conv_args(f.packed, f.L, CV_P, C, B, h, w, h, w, f.xb, C, nullptr, 0);
-            a.out0 = f.z; a.aux0 = f.z; a.lambda = blob<float>(f.packed, f.L.lambda);
+            a = conv_args(f.packed, f.L, CV_P, C, B, h, w, h, w, f.xs ? f.xs + it * hw * C : f.xb, C,
+                          nullptr, 0);
+            a.out0 = f.z; a.aux0 = zl_in ? f.zl : f.z; a.lambda = blob<float>(f.packed, f.L.lambda);
+            a.out1 = f.v ? f.v + it * hw * 2 * C : nullptr;
             return launch_conv<STAGE_S1, EPI_ISTA_P, 1>(a, f.st);
         case CISTA_LAYER_DG:        // y = relu(Dg.conv(z))                      base_layers.py:222
             a = conv_args(f.packed, f.L, CV_DG, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
-            a.out0 = f.xb;
+            a.out0 = f.y ? f.y : f.xb;
             return launch_conv<STAGE_S1, EPI_RELU, 1>(a, f.st);
         case CISTA_LAYER_LSTM:      // ConvLSTM on cat(y, h_prev)                  :112-128
-            a = conv_args(f.packed, f.L, CV_LSTM, C, B, h, w, h, w, f.xb, C, f.h_prev, C);
-            a.out0 = f.hs; a.out1 = f.cs; a.aux0 = f.c_prev;
+            a = conv_args(f.packed, f.L, CV_LSTM, C, B, h, w, h, w, f.y ? f.y : f.xb, C, f.h_prev, C);
+            a.out0 = f.hs; a.out1 = f.cs; a.aux0 = f.c_prev; a.out2 = f.lg;
             return launch_conv<STAGE_S1, EPI_LSTM, 4>(a, f.st);
         case CISTA_LAYER_UPSAMPLE:  // relu(conv(ReflectionPad(up2x(h))))          :193-210
             a = conv_args(f.packed, f.L, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
             a.out0 = f.full;
             if (up_q_path(C)) {     // + final_conv's channel contraction in the epilogue
                 a.aux0 = blob<float>(f.packed, f.L.wF);
+                a.out1 = f.u;
                 return launch_conv<STAGE_UP, EPI_UP_Q, 1>(a, f.st);
             }
             return launch_conv<STAGE_UP, EPI_RELU, 1>(a, f.st);
@@ -394,8 +417,8 @@ int run_layers(const Frame &f, const int *layers, int n) {
 
 int run_ista(const Frame &f, int iters) {
     for (int i = 0; i < iters; ++i) {                                  // e2v_model.py:72-78
-        CHECK(run_layer(f, CISTA_LAYER_ISTA_D));
-        CHECK(run_layer(f, CISTA_LAYER_ISTA_P));
+        CHECK(run_layer(f, CISTA_LAYER_ISTA_D, i));
+        CHECK(run_layer(f, CISTA_LAYER_ISTA_P, i));
     }
     return CISTA_OK;
 }
@@ -424,6 +447,348 @@ int check_common(const cista_config *cfg, const void *packed, int B, int H, int 
     return CISTA_OK;
 }
 
+
+// =========================================================================================
+// training: saved activations, backward workspace, backward schedule
+// =========================================================================================
+struct Saved {
+    float *x1, *z0, *gi, *gf, *go, *zl, *v, *xs, *y, *lg, *u;
+    size_t bytes;
+};
+
+Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
+    const size_t hw = (size_t)B * (H / 2) * (W / 2), HW = (size_t)B * H * W;
+    const int C = cfg.base_channels, D = cfg.depth;
+    Saved s;
+    size_t off = 0;
+    char *base = static_cast<char *>(buf);
+    auto take = [&](size_t nfloat) {
+        float *p = reinterpret_cast<float *>(base + off);
+        off = align_up(off + nfloat * 4);
+        return p;
+    };
+    s.x1 = take(hw * C);
+    s.z0 = take(hw * 2 * C);
+    s.gi = take(hw * 2 * C);
+    s.gf = take(hw * 2 * C);
+    s.go = take(hw * 2 * C);
+    s.zl = take(hw * 2 * C);
+    s.v = take(hw * 2 * C * (D > 0 ? D : 1));
+    s.xs = take(hw * C * (D > 0 ? D : 1));
+    s.y = take(hw * C);
+    s.lg = take(hw * 4 * C);
+    s.u = take(HW * C);
+    s.bytes = off;
+    return s;
+}
+
+constexpr int WG_SPLIT_MAX = 64;
+
+struct BwdWs {
+    float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
+    float *part, *dlp;
+    unsigned *amax;     // [8] absmax bits
+    float *scl;         // [16] scale pairs
+    size_t bytes;
+};
+
+BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
+    const int h = H / 2, w = W / 2, C = cfg.base_channels;
+    const size_t hw = (size_t)B * h * w, HW = (size_t)B * H * W;
+    BwdWs s;
+    size_t off = 0;
+    char *base = static_cast<char *>(buf);
+    auto take = [&](size_t nfloat) {
+        float *p = reinterpret_cast<float *>(base + off);
+        off = align_up(off + nfloat * 4);
+        return p;
+    };
+    s.gpre = take(HW);
+    s.gU = take(HW * C);
+    s.dxpF = take((size_t)B * (H + 2) * (W + 2) * C);
+    s.ghb = take(hw * C);
+    s.Gl = take(hw * 4 * C);
+    s.dxp = take((size_t)B * (h + 2) * (w + 2) * 4 * C);
+    s.gy = take(hw * C);
+    s.gz = take(hw * 2 * C);
+    s.gv = take(hw * 2 * C);
+    s.gxk = take(hw * C);
+    s.zk = take(hw * 2 * C);
+    s.gx1 = take(hw * C);
+    s.Go = take(hw * 2 * C);
+    s.gz0 = take(hw * 2 * C);
+    s.part = take((size_t)WG_SPLIT_MAX * (4 * C) * (4 * C) * 9);
+    s.dlp = take((size_t)2 * C * 512);
+    s.amax = reinterpret_cast<unsigned *>(take(16));
+    s.scl = take(32);
+    s.bytes = off;
+    return s;
+}
+
+inline dim3 g1d(long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+// per-tensor power-of-two scale for an fp16-split dgrad input: {s, 1/s} -> scl
+__global__ void absmax_kernel(const float *x, long n, unsigned *amax) {
+    __shared__ float red[256];
+    float m = 0.0f;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
+    red[threadIdx.x] = m;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + k]);
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) atomicMax(amax, __float_as_uint(red[0]));
+}
+
+__global__ void scale_from_amax_kernel(const unsigned *amax, float *scl) {
+    const float mx = __uint_as_float(*amax);
+    int e = 0;
+    if (mx > 0.0f && isfinite(mx)) {
+        e = (int)floorf(log2f(16384.0f / mx));
+        e = e < -60 ? -60 : (e > 60 ? 60 : e);
+    }
+    scl[0] = ldexpf(1.0f, e);
+    scl[1] = ldexpf(1.0f, -e);
+}
+
+struct Bwd {
+    const cista_config *cfg;
+    const void *packed;
+    Layout L;
+    int B, H, W, h, w, C;
+    hipStream_t st;
+    BwdWs ws;
+    int slot;   // rotating scale slot
+};
+
+int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
+
+// dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor
+template <int XS>
+int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, int x0c,
+          const float *X1, int x1c, int Cin, int Hin, int Win, int Hout, int Wout, float *dst,
+          float sign, int accumulate) {
+    WgradArgs a;
+    memset(&a, 0, sizeof(a));
+    a.G = G; a.Gc = Gc; a.Goff = Goff;
+    a.X0 = X0; a.x0c = x0c; a.X1 = X1; a.x1c = x1c;
+    a.B = k.B; a.Hin = Hin; a.Win = Win; a.Hout = Hout; a.Wout = Wout;
+    const int T = XS == XS_S2 ? 8 : 16;
+    a.TH = Hout < T ? Hout : T;
+    a.TW = Wout < T ? Wout : T;
+    a.tiles_y = (Hout + a.TH - 1) / a.TH;
+    a.tiles_x = (Wout + a.TW - 1) / a.TW;
+    a.Cout = Cout; a.Cin = Cin;
+    const int nblk = ((Cout + 31) / 32) * ((Cin + 31) / 32);
+    const int ntiles = k.B * a.tiles_y * a.tiles_x;
+    int ns = (2048 + nblk - 1) / nblk;
+    ns = ns > WG_SPLIT_MAX ? WG_SPLIT_MAX : ns;
+    ns = ns > ntiles ? ntiles : ns;
+    ns = ns < 1 ? 1 : ns;
+    a.nsplit = ns;
+    a.partial = k.ws.part;
+    constexpr int S = XS == XS_S2 ? 2 : 1;
+    const int HP = ((a.TH - 1) * S + 3) * ((a.TW - 1) * S + 3);
+    const size_t lds = ((size_t)((a.TH * a.TW + 3) & ~3) + HP) * 33 * 4;
+    auto kern = wgrad_kernel<XS>;
+    if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
+    hipLaunchKernelGGL(kern, dim3(nblk, ns), dim3(256), lds, k.st, a);
+    const long n = (long)Cout * Cin * 9;
+    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
+                       dst, sign, accumulate);
+    return hip_ok();
+}
+
+int bias_grad(Bwd &k, const float *G, int Gc, int Goff, int n, long npix, float *dst, float sign,
+              int accumulate) {
+    int ns = (int)((npix + 4095) / 4096);
+    ns = ns < 1 ? 1 : (ns > 256 ? 256 : ns);
+    hipLaunchKernelGGL(channel_sum_kernel, dim3((n + 63) / 64, ns), dim3(256), 0, k.st, G, Gc, Goff, n, npix,
+                       k.ws.part);
+    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, (long)n,
+                       dst, sign, accumulate);
+    return hip_ok();
+}
+
+// dxp (B, h+2, w+2, N) = padded-domain gradient of conv `id`'s input, from G (B,h,w,K)
+int dgrad_conv(Bwd &k, int id, const float *G, float *dxp) {
+    const ConvShape s = conv_shape(id, k.C);
+    const int Hin = id == CV_UP ? k.H : k.h, Win = id == CV_UP ? k.W : k.w;
+    const long n = (long)k.B * Hin * Win * s.cout;
+    unsigned *am = k.ws.amax + (k.slot & 7);
+    float *sc = k.ws.scl + 2 * (k.slot & 7);
+    ++k.slot;
+    if (hipMemsetAsync(am, 0, 4, k.st) != hipSuccess) return CISTA_ERR_HIP;
+    hipLaunchKernelGGL(absmax_kernel, dim3(512), dim3(256), 0, k.st, G, n, am);
+    hipLaunchKernelGGL(scale_from_amax_kernel, dim3(1), dim3(1), 0, k.st, (const unsigned *)am, sc);
+    ConvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in0 = G; a.c0 = s.cout; a.in1 = nullptr; a.c1 = 0;
+    a.B = k.B; a.Hin = Hin; a.Win = Win; a.Hout = Hin + 2; a.Wout = Win + 2;
+    a.wpack = blob<u32x4>(k.packed, k.L.dwp[id]);
+    a.bias = blob<float>(k.packed, k.L.dbp[id]);
+    a.wscale = blob<float>(k.packed, k.L.sc[id]) + 1;
+    a.ascale = sc;
+    a.N = s.cin; a.Cout = s.cin;
+    a.out0 = dxp;
+    return launch_conv<STAGE_ZP2, EPI_BIAS, 1>(a, k.st);
+}
+
+int fold(Bwd &k, const float *src, int Cs, int sc0, float *dst, int Cd, int dc0, int n, int H, int W,
+         float scale, int accumulate, const float *mask) {
+    FoldArgs f;
+    f.src = src; f.Cs = Cs; f.sc0 = sc0; f.dst = dst; f.Cd = Cd; f.dc0 = dc0; f.n = n;
+    f.B = k.B; f.H = H; f.W = W; f.scale = scale; f.accumulate = accumulate; f.mask = mask;
+    hipLaunchKernelGGL(fold_reflect_kernel, g1d((long)k.B * H * W * (n / 4)), dim3(256), 0, k.st, f);
+    return hip_ok();
+}
+
+int copy_or_zero(float *dst, const float *src, size_t nfloat, hipStream_t st) {
+    const hipError_t e = src ? hipMemcpyAsync(dst, src, nfloat * 4, hipMemcpyDeviceToDevice, st)
+                             : hipMemsetAsync(dst, 0, nfloat * 4, st);
+    return e == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+}
+
+int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const Saved &sv,
+                 const cista_grad_io &g, const cista_param_grads &pg) {
+    const int B = k.B, H = k.H, W = k.W, h = k.h, w = k.w, C = k.C, D = k.cfg->depth;
+    const long hw = (long)B * h * w, HW = (long)B * H * W;
+    BwdWs &ws = k.ws;
+    hipStream_t st = k.st;
+    // ---- 1-2. output stage: rec = sigmoid(final_conv(u)), u = relu(upsamp_conv(up(h))) --------
+    CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
+    if (g.g_rec) {
+        hipLaunchKernelGGL(sigmoid_bwd_kernel, g1d(HW), dim3(256), 0, st, g.g_rec, io.rec, ws.gpre, HW);
+        CHECK(bias_grad(k, ws.gpre, 1, 0, 1, HW, pg.final_b, 1.0f, 0));
+        CHECK(wgrad<XS_S1>(k, ws.gpre, 1, 0, 1, sv.u, C, nullptr, 0, C, H, W, H, W, pg.final_w, 1.0f, 0));
+        DgradSmallArgs d;
+        d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
+        d.mask = sv.u; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = 1; d.Cin = C;
+        d.accumulate = 0;
+        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * C), dim3(256), 0, st, d);   // g_U (ReLU'd)
+        CHECK(bias_grad(k, ws.gU, C, 0, C, HW, pg.up_b, 1.0f, 0));
+        CHECK(wgrad<XS_UP>(k, ws.gU, C, 0, C, io.h, C, nullptr, 0, C, h, w, H, W, pg.up_w, 1.0f, 0));
+        CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF));
+        CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
+        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
+                           B, h, w, C, 1);
+    } else {
+        if (hipMemsetAsync(pg.final_b, 0, 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.final_w, 0, (size_t)9 * C * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.up_b, 0, (size_t)C * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.up_w, 0, (size_t)9 * C * C * 4, st) != hipSuccess)
+            return CISTA_ERR_HIP;
+    }
+    // ---- 3. ConvLSTM ---------------------------------------------------------------------
+    hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
+                       io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C);
+    CHECK(bias_grad(k, ws.Gl, 4 * C, 0, 4 * C, hw, pg.lstm_b, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0));
+    CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp));
+    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y));        // relu(Dg) mask
+    if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
+    // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
+    CHECK(bias_grad(k, ws.gy, C, 0, C, hw, pg.Dg_b, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0));
+    CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp));
+    CHECK(copy_or_zero(ws.gz, g.g_z, (size_t)hw * 2 * C, st));
+    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    // ---- 5. ISTA, reversed (tied D, P, lambda accumulate over iterations) -------------------
+    const float *lam = blob<float>(k.packed, k.L.lambda);
+    if (D == 0) {
+        if (hipMemsetAsync(pg.lambda, 0, (size_t)2 * C * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.D_w, 0, (size_t)C * 2 * C * 9 * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.D_b, 0, (size_t)C * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.P_w, 0, (size_t)2 * C * C * 9 * 4, st) != hipSuccess ||
+            hipMemsetAsync(pg.P_b, 0, (size_t)2 * C * 4, st) != hipSuccess)
+            return CISTA_ERR_HIP;
+    }
+    if (hipMemsetAsync(ws.gx1, 0, (size_t)hw * C * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+    const int nbl = 512;   // softshrink_bwd blocks (lambda partials [nbl][2C])
+    for (int it = D - 1; it >= 0; --it) {
+        const float *v = sv.v + (size_t)it * hw * 2 * C;
+        const float *xk = sv.xs + (size_t)it * hw * C;
+        const float *zk = sv.zl;
+        if (it > 0) {
+            hipLaunchKernelGGL(softshrink_fwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st,
+                               sv.v + (size_t)(it - 1) * hw * 2 * C, lam, ws.zk, hw, 2 * C);
+            zk = ws.zk;
+        }
+        hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
+                           lam, ws.gv, ws.dlp, hw, 2 * C);
+        // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
+        // P: v = z_k + P(x_k) + b_P
+        CHECK(bias_grad(k, ws.gv, 2 * C, 0, 2 * C, hw, pg.P_b, 1.0f, it != D - 1));
+        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1));
+        CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp));
+        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr));
+        CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+        // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
+        CHECK(bias_grad(k, ws.gxk, C, 0, C, hw, pg.D_b, -1.0f, it != D - 1));
+        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1));
+        CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp));
+        CHECK(copy_or_zero(ws.gz, ws.gv, (size_t)hw * 2 * C, st));          // identity path
+        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 1, nullptr));
+        // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
+        hipLaunchKernelGGL(lambda_grad_kernel, dim3(1), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
+                           pg.lambda, it != D - 1);
+    }
+    // ---- 6. ConvLSTC --------------------------------------------------------------------------
+    // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part)
+    hipLaunchKernelGGL(lstc_bwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st, (const float *)sv.gi,
+                       (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
+                       (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
+                       ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C);
+    CHECK(bias_grad(k, ws.Go, 2 * C, 0, 2 * C, hw, pg.out_gates_b, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
+                       pg.out_gates_w, 1.0f, 0));
+    CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp));
+    CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    const bool want_zp = io.z_prev && g.g_z_prev;
+    if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
+    CHECK(bias_grad(k, ws.Gl, 4 * C, 0, 4 * C, hw, pg.gates_b, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
+                       pg.gates_w, 1.0f, 0));
+    CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp));
+    CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+    if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    CHECK(bias_grad(k, ws.gz0, 2 * C, 0, 2 * C, hw, pg.P0_b, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0));
+    CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp));
+    CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+    // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
+    float *xfull = ws.gU, *gxfull = ws.dxpF;
+    {
+        Frame f;
+        memset(&f, 0, sizeof(f));
+        f.cfg = k.cfg; f.packed = k.packed; f.L = k.L; f.B = B; f.H = H; f.W = W; f.h = h; f.w = w;
+        f.C = C; f.events = io.events; f.prev_image = io.prev_image; f.full = xfull; f.st = st;
+        CHECK(run_layer(f, CISTA_LAYER_INPUT));
+    }
+    CHECK(bias_grad(k, ws.gx1, C, 0, C, hw, pg.W0_b, 1.0f, 0));
+    CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0));
+    {
+        DgradSmallArgs d;
+        d.G = ws.gx1; d.Gc = C; d.Goff = 0; d.W = P.W0_w; d.dX = gxfull; d.Xc = C; d.Xoff = 0; d.mask = nullptr;
+        d.B = B; d.Hin = H; d.Win = W; d.Hout = h; d.Wout = w; d.S = 2; d.Cout = C; d.Cin = C; d.accumulate = 0;
+        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * C), dim3(256), 0, st, d);
+    }
+    // ---- 8. We / Wi ----------------------------------------------------------------------------
+    const int half = C / 2, nb = k.cfg->num_bins;
+    CHECK(bias_grad(k, gxfull, C, 0, half, HW, pg.We_b, 1.0f, 0));
+    CHECK(bias_grad(k, gxfull, C, half, half, HW, pg.Wi_b, 1.0f, 0));
+    CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0));
+    CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0));
+    if (g.g_prev_image) {
+        DgradSmallArgs d;
+        d.G = gxfull; d.Gc = C; d.Goff = half; d.W = P.Wi_w; d.dX = g.g_prev_image; d.Xc = 0; d.Xoff = 0;
+        d.mask = nullptr; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = half;
+        d.Cin = 1; d.accumulate = 0;
+        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW), dim3(256), 0, st, d);
+    }
+    return hip_ok();
+}
 }  // namespace
 
 // =========================================================================================
@@ -476,6 +841,14 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
         a.Cout = s.cout; a.Cin = s.cin; a.G = s.G;
         const long total = (long)(s.cin / 32) * 9 * (s.cout / 16) * 64;
         hipLaunchKernelGGL(pack_conv_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, a);
+        // dgrad pack: K = forward Cout, N = forward Cin, same scale
+        PackArgs d = a;
+        d.wp = blobw<u32x4>(packed, L.dwp[i]);
+        d.bp = blobw<float>(packed, L.dbp[i]);
+        d.Cout = s.cin; d.Cin = s.cout;
+        const long dtotal = (long)(s.cout / 32) * 9 * (s.cin / 16) * 64;
+        const long dgrid = dtotal > s.cin ? dtotal : s.cin;
+        hipLaunchKernelGGL(pack_dgrad_kernel, dim3((unsigned)((dgrid + 255) / 256)), dim3(256), 0, st, d);
     }
     const int half = C / 2;
     hipLaunchKernelGGL(transpose_small_kernel, dim3((half * nb * 9 + 255) / 256), dim3(256), 0, st,
@@ -611,4 +984,72 @@ int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, i
     return run_layer(f, layer);
 }
 
+
+size_t cista_saved_bytes(const cista_config *cfg, int B, int H, int W) {
+    if (!cfg_ok(cfg) || B <= 0 || H <= 0 || W <= 0) return 0;
+    return carve_saved(nullptr, *cfg, B, H, W).bytes;
+}
+
+size_t cista_train_workspace_bytes(const cista_config *cfg, int B, int H, int W) {
+    if (!cfg_ok(cfg) || B <= 0 || H <= 0 || W <= 0) return 0;
+    const size_t a = carve(nullptr, B, H, W, cfg->base_channels).bytes;
+    const size_t b = carve_bwd(nullptr, *cfg, B, H, W).bytes;
+    return a > b ? a : b;
+}
+
+static int train_supported(const cista_config *cfg) {
+    return (cfg->base_channels == 64 || cfg->base_channels == 32) ? CISTA_OK : CISTA_ERR_UNSUPPORTED;
+}
+
+int cista_forward_train(const cista_config *cfg, const void *packed, int B, int H, int W,
+                        const cista_frame_io *io, void *saved, size_t saved_bytes, void *workspace,
+                        size_t workspace_bytes, void *stream) {
+    CHECK(check_common(cfg, packed, B, H, W));
+    CHECK(train_supported(cfg));
+    if (!io || !io->events || !io->prev_image || !io->rec || !io->c_lstc || !io->z || !io->h ||
+        !io->c || !workspace || !saved)
+        return CISTA_ERR_INVALID;
+    if ((H & 1) || (W & 1) || H < 4 || W < 4) return CISTA_ERR_INVALID;
+    if ((io->h_prev == nullptr) != (io->c_prev == nullptr)) return CISTA_ERR_INVALID;
+    if (workspace_bytes < carve(nullptr, B, H, W, cfg->base_channels).bytes) return CISTA_ERR_WORKSPACE;
+    const Saved sv = carve_saved(saved, *cfg, B, H, W);
+    if (saved_bytes < sv.bytes) return CISTA_ERR_WORKSPACE;
+    Frame f = make_frame(cfg, packed, B, H, W, workspace, stream);
+    bind_io(f, io);
+    f.x1 = sv.x1; f.z0 = sv.z0; f.gi = sv.gi; f.gf = sv.gf; f.go = sv.go; f.zl = sv.zl;
+    f.v = sv.v; f.xs = sv.xs; f.y = sv.y; f.lg = sv.lg; f.u = sv.u;
+    static const int head[] = {CISTA_LAYER_INPUT, CISTA_LAYER_W0, CISTA_LAYER_P0, CISTA_LAYER_GATES,
+                               CISTA_LAYER_OUT_GATES};
+    static const int tail[] = {CISTA_LAYER_DG, CISTA_LAYER_LSTM, CISTA_LAYER_UPSAMPLE, CISTA_LAYER_FINAL};
+    CHECK(run_layers(f, head, 5));
+    CHECK(run_ista(f, cfg->depth));
+    return run_layers(f, tail, 4);
+}
+
+int cista_backward(const cista_config *cfg, const void *packed, const cista_params *params, int B,
+                   int H, int W, const cista_frame_io *io, const void *saved, size_t saved_bytes,
+                   const cista_grad_io *grads, const cista_param_grads *pg, void *workspace,
+                   size_t workspace_bytes, void *stream) {
+    CHECK(check_common(cfg, packed, B, H, W));
+    CHECK(train_supported(cfg));
+    if (!params || !io || !saved || !grads || !pg || !workspace) return CISTA_ERR_INVALID;
+    if (!params->W0_w || !params->final_w || !params->Wi_w) return CISTA_ERR_INVALID;
+    const void *req[] = {pg->We_w, pg->We_b, pg->Wi_w, pg->Wi_b, pg->W0_w, pg->W0_b, pg->gates_w,
+                         pg->gates_b, pg->out_gates_w, pg->out_gates_b, pg->P0_w, pg->P0_b, pg->lambda,
+                         pg->D_w, pg->D_b, pg->P_w, pg->P_b, pg->Dg_w, pg->Dg_b, pg->lstm_w, pg->lstm_b,
+                         pg->up_w, pg->up_b, pg->final_w, pg->final_b};
+    for (const void *q : req)
+        if (!q) return CISTA_ERR_INVALID;
+    if ((H & 1) || (W & 1) || H < 4 || W < 4) return CISTA_ERR_INVALID;
+    const Saved sv = carve_saved(const_cast<void *>(saved), *cfg, B, H, W);
+    if (saved_bytes < sv.bytes) return CISTA_ERR_WORKSPACE;
+    Bwd k;
+    k.cfg = cfg; k.packed = packed; k.L = make_layout(*cfg);
+    k.B = B; k.H = H; k.W = W; k.h = H / 2; k.w = W / 2; k.C = cfg->base_channels;
+    k.st = static_cast<hipStream_t>(stream);
+    k.ws = carve_bwd(workspace, *cfg, B, H, W);
+    k.slot = 0;
+    if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
+    return run_backward(k, *params, *io, sv, *grads, *pg);
+}
 }  // extern "C"

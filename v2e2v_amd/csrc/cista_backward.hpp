@@ -1,0 +1,471 @@
+// cista_backward.hpp -- BPTT backward kernels of the CISTA-LSTC frame (SURVEY section 8 row a11;
+// reference train_e2v.py:108-130 drives autograd through e2v/e2v_model.py:41-90).
+//
+//  * dgrad of the MFMA-sized reflect-padded convs reuses conv3x3_split3 with STAGE_ZP2: a
+//    correlation of the zero-padded output gradient with the flipped, transposed weights
+//    (packed by pack_dgrad_kernel) produces the gradient on the PADDED input domain, which
+//    fold_reflect_kernel folds back (padded index -1 -> 1, H -> H-2) and accumulates;
+//  * wgrad is a pixel-reduction GEMM on exact fp32 MFMA (v_mfma_f32_16x16x4f32): per pixel tile
+//    the output gradient and the reflect-padded input halo are staged in LDS, every wave owns
+//    one 16x16 (cout x cin) block for all 9 taps; per-split partial sums are reduced by
+//    reduce_partials_kernel (deterministic, no atomics);
+//  * the elementwise tails (sigmoid/tanh gate algebra, softshrink, ReLU masks, bilinear x2,
+//    the final 64->1 conv) have dedicated fp32 kernels.
+#pragma once
+#include "cista_kernels.hpp"
+
+namespace cista {
+
+// --------------------------------------------------------------------------------------------
+// fold the padded-domain gradient of a reflect-padded (pad 1) conv back onto its input:
+// dst[b,y,x,dc0+c] (+)= scale * sum of src[b, Y, X, sc0+c] over padded (Y, X) whose reflected
+// index is (y, x).  src is (B, H+2, W+2, Cs); dst (B, H, W, Cd).  Optional ReLU-style mask:
+// multiply by (mask[b,y,x,c] > 0) after accumulation (mask NHWC with Cd channels).
+// --------------------------------------------------------------------------------------------
+struct FoldArgs {
+    const float *src; int Cs, sc0;
+    float *dst; int Cd, dc0;
+    int n;                 // channels folded
+    int B, H, W;
+    float scale;
+    int accumulate;        // 0: dst = fold, 1: dst += fold
+    const float *mask;     // optional, applied to the result (NHWC, Cd channels)
+};
+
+__device__ __forceinline__ int refl_sources(int i, int n, int (&out)[3]) {
+    // padded indices P in [0, n+2) with reflect(P - 1) == i, i.e. the padded positions that
+    // read input index i: P = i + 1, plus P = 0 when i == 1 and P = n + 1 when i == n - 2
+    int k = 0;
+    out[k++] = i + 1;
+    if (i == 1) out[k++] = 0;
+    if (i == n - 2) out[k++] = n + 1;
+    return k;
+}
+
+__global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
+    const int g4 = a.n / 4;
+    const long total = (long)a.B * a.H * a.W * g4;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int c = (int)(idx % g4) * 4;
+    const long pix = idx / g4;
+    const int x = (int)(pix % a.W);
+    const int y = (int)((pix / a.W) % a.H);
+    const int b = (int)(pix / ((long)a.W * a.H));
+    int ys[3], xs[3];
+    const int ny = refl_sources(y, a.H, ys), nx = refl_sources(x, a.W, xs);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < ny; ++i)
+        for (int j = 0; j < nx; ++j) {
+            const float4 v = *(const float4 *)(a.src + (((size_t)b * (a.H + 2) + ys[i]) * (a.W + 2) + xs[j]) * a.Cs + a.sc0 + c);
+            s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
+        }
+    float4 *d = (float4 *)(a.dst + (size_t)pix * a.Cd + a.dc0 + c);
+    float4 r = make_float4(s.x * a.scale, s.y * a.scale, s.z * a.scale, s.w * a.scale);
+    if (a.accumulate) {
+        const float4 o = *d;
+        r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    }
+    if (a.mask) {
+        const float4 m = *(const float4 *)(a.mask + (size_t)pix * a.Cd + a.dc0 + c);
+        r.x = m.x > 0.f ? r.x : 0.f; r.y = m.y > 0.f ? r.y : 0.f;
+        r.z = m.z > 0.f ? r.z : 0.f; r.w = m.w > 0.f ? r.w : 0.f;
+    }
+    *d = r;
+}
+
+// dgrad weight packing: B fragment of the dgrad conv = W[k=cout][col=cin] at the flipped tap
+// (t' = 8 - t), same [kc][tap][ntile][part][lane] layout and per-layer scale as the forward.
+__global__ void pack_dgrad_kernel(const PackArgs a) {
+    // here a.Cin = forward Cout (the dgrad K), a.Cout = forward Cin (the dgrad N)
+    const int NT = a.Cout / 16;
+    const int KC = a.Cin / 32;
+    const long total = (long)KC * 9 * NT * 64;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < a.Cout) a.bp[idx] = 0.0f;
+    if (idx >= total) return;
+    const int lane = (int)(idx % 64);
+    long r = idx / 64;
+    const int nt = (int)(r % NT);
+    r /= NT;
+    const int tap = (int)(r % 9);
+    const int kc = (int)(r / 9);
+    const int ci_fwd = nt * 16 + (lane & 15);        // dgrad output channel = forward input channel
+    const float s = a.scale[0];
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int co_fwd = kc * 32 + 8 * (lane >> 4) + j;
+        // forward weight layout [co][ci][ky][kx], a.Cin (= fwd Cout) rows of a.Cout (= fwd Cin)
+        const float v = a.w[((size_t)co_fwd * a.Cout + ci_fwd) * 9 + (8 - tap)] * s;
+        const _Float16 hb = (_Float16)v;
+        h[j] = hb;
+        l[j] = (_Float16)(v - (float)hb);
+    }
+    const size_t base = ((((size_t)kc * 9 + tap) * NT + nt) * 2) * 64 + lane;
+    a.wp[base] = __builtin_bit_cast(u32x4, h);
+    a.wp[base + 64] = __builtin_bit_cast(u32x4, l);
+}
+
+// --------------------------------------------------------------------------------------------
+// wgrad: dW[co][ci][t] (+)= sign * sum_P G(P, co) * Xpad(S*P + t, ci) on exact fp32 MFMA.
+// --------------------------------------------------------------------------------------------
+enum XStage { XS_S1 = 0, XS_S2 = 1, XS_UP = 2, XS_NCHW = 3 };
+
+struct WgradArgs {
+    const float *G; int Gc, Goff;       // output gradient NHWC (B, Hout, Wout, Gc); cout j at Goff + j
+    const float *X0; int x0c;           // input segment 0 (NHWC, or NCHW planes for XS_NCHW)
+    const float *X1; int x1c;           // input segment 1 (may be NULL: zeros)
+    int B, Hin, Win, Hout, Wout;        // XS_UP: Hin/Win = half-res source, Hout = 2 Hin
+    int TH, TW, tiles_x, tiles_y;
+    int Cout, Cin;                      // forward conv shape
+    int nsplit;
+    float *partial;                     // [nsplit][Cout][Cin][9]
+};
+
+typedef float f32x4w __attribute__((ext_vector_type(4)));
+
+template <int XS>
+__device__ __forceinline__ float wg_load_x(const WgradArgs &a, int b, int iy, int ix, int ci) {
+    // one input value of the (virtual) reflect-padded conv input; 0 beyond Cin
+    if (ci >= a.Cin) return 0.0f;
+    const float *seg = ci < a.x0c ? a.X0 : a.X1;
+    const int segC = ci < a.x0c ? a.x0c : a.x1c;
+    const int cc = ci < a.x0c ? ci : ci - a.x0c;
+    if (!seg) return 0.0f;
+    if constexpr (XS == XS_UP) {
+        const int Hu = 2 * a.Hin, Wu = 2 * a.Win;
+        const int Y = reflect_clamp(iy, Hu), X = reflect_clamp(ix, Wu);
+        float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
+        float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const int y0 = (int)sy, x0 = (int)sx;
+        const int y1 = y0 + (y0 < a.Hin - 1 ? 1 : 0), x1 = x0 + (x0 < a.Win - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1, lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+        const float *base = seg + (size_t)b * a.Hin * a.Win * segC + cc;
+        const float v00 = base[((size_t)y0 * a.Win + x0) * segC], v01 = base[((size_t)y0 * a.Win + x1) * segC];
+        const float v10 = base[((size_t)y1 * a.Win + x0) * segC], v11 = base[((size_t)y1 * a.Win + x1) * segC];
+        return ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+    } else if constexpr (XS == XS_NCHW) {
+        const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
+        return seg[(((size_t)b * segC + cc) * a.Hin + y) * a.Win + x];
+    } else {
+        const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
+        return seg[(((size_t)b * a.Hin + y) * a.Win + x) * segC + cc];
+    }
+}
+
+// workgroup: 4 waves = 2 (cout 16-blocks) x 2 (cin 16-blocks); blockIdx.x = (co32, ci32) block,
+// blockIdx.y = split; the split loops over pixel tiles t = split, split + nsplit, ...
+template <int XS>
+__global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
+    extern __shared__ float wsm[];
+    constexpr int S = XS == XS_S2 ? 2 : 1;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int nci = (a.Cin + 31) / 32;
+    const int co0 = (blockIdx.x / nci) * 32, ci0 = (blockIdx.x % nci) * 32;
+    const int wco = (wave >> 1) * 16, wci = (wave & 1) * 16;
+    const int TH = a.TH, TW = a.TW;
+    const int HWd = (TW - 1) * S + 3, HH = (TH - 1) * S + 3;
+    const int HP = HH * HWd;
+    const int NPX = TH * TW;
+    const int NPX4 = (NPX + 3) & ~3;
+    float *Gs = wsm;                       // [NPX4][33]
+    float *Xs = wsm + NPX4 * 33;           // [HP][33]
+    f32x4w acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = f32x4w{0.f, 0.f, 0.f, 0.f};
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * TH, ox0 = tx * TW;
+        __syncthreads();
+        // stage G tile (zero outside the image / beyond Cout)
+        for (int i = threadIdx.x; i < NPX4 * 32; i += 256) {
+            const int p = i >> 5, c = i & 31;
+            const int py = p / TW, px = p - py * TW;
+            const int oy = oy0 + py, ox = ox0 + px;
+            float v = 0.0f;
+            if (p < NPX && oy < a.Hout && ox < a.Wout && co0 + c < a.Cout)
+                v = a.G[(((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + c];
+            Gs[p * 33 + c] = v;
+        }
+        // stage the input halo
+        const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+        for (int i = threadIdx.x; i < HP * 32; i += 256) {
+            const int hp = i >> 5, c = i & 31;
+            const int hy = hp / HWd, hx = hp - hy * HWd;
+            Xs[hp * 33 + c] = wg_load_x<XS>(a, b, iy0 + hy, ix0 + hx, ci0 + c);
+        }
+        __syncthreads();
+        for (int p4 = 0; p4 < NPX4; p4 += 4) {
+            const int p = p4 + (lane >> 4);
+            const float av = Gs[p * 33 + wco + (lane & 15)];
+            const int pp = p < NPX ? p : NPX - 1;
+            const int py = pp / TW, px = pp - py * TW;
+            const int hb = (py * S) * HWd + px * S;
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const float bv = Xs[(hb + (t / 3) * HWd + (t % 3)) * 33 + wci + (lane & 15)];
+                acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
+            }
+        }
+    }
+    // acc[t][j]: row (cout) 4*(lane>>4) + j, col (cin) lane & 15
+    float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int co = co0 + wco + 4 * (lane >> 4) + j;
+        const int ci = ci0 + wci + (lane & 15);
+        if (co < a.Cout && ci < a.Cin)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[t][j];
+    }
+}
+
+// dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9)
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float *partial, int nsplit, long n,
+                                                              float *dst, float sign, int accumulate) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.0f;
+    for (int k = 0; k < nsplit; ++k) s += partial[(size_t)k * n + i];
+    dst[i] = (accumulate ? dst[i] : 0.0f) + sign * s;
+}
+
+// per-channel pixel sums, phase 1: grid (ceil(n/64), nsplit); block = 64 channels x 4 pixel
+// rows; partial[split][c] = sum over the split's pixels of G[p][Goff + c]
+__global__ __launch_bounds__(256) void channel_sum_kernel(const float *G, int Gc, int Goff, int n, long npix,
+                                                          float *partial) {
+    __shared__ float red[4][64];
+    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int r = threadIdx.x >> 6;
+    const long step = (long)gridDim.y * 4;
+    float s = 0.0f;
+    if (c < n)
+        for (long p = (long)blockIdx.y * 4 + r; p < npix; p += step) s += G[(size_t)p * Gc + Goff + c];
+    red[r][threadIdx.x & 63] = s;
+    __syncthreads();
+    if (r == 0 && c < n)
+        partial[(size_t)blockIdx.y * n + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
+                                              red[3][threadIdx.x];
+}
+
+// --------------------------------------------------------------------------------------------
+// generic VALU dgrad of a small reflect-padded 3x3 conv with stride S (W0, final_conv, Wi):
+// dX[b,Q,ci] (+)= sum over (P, t) with reflect(S*P + t - 1) == Q of G[b,P,co] W[co][ci][t]
+// G NHWC (B, Hout, Wout, Gc) channels [Goff, Goff+Cout); dX layout NHWC (Xc, Xoff) or, for
+// Xc == 0, NCHW planes with Cin == 1 (prev_image).
+// --------------------------------------------------------------------------------------------
+struct DgradSmallArgs {
+    const float *G; int Gc, Goff;
+    const float *W;       // [Cout][Cin][3][3]
+    float *dX; int Xc, Xoff;
+    const float *mask;    // optional: dX *= (mask > 0), mask laid out like dX
+    int B, Hin, Win, Hout, Wout, S, Cout, Cin;
+    int accumulate;
+};
+
+__device__ __forceinline__ int refl_taps(int q, int n_in, int n_out, int S, int (&P)[6], int (&T)[6]) {
+    // all (P, t) with reflect(S*P + t - 1) == q, 0 <= P < n_out, t in 0..2
+    int k = 0;
+    const int lo = (q - 2) / S - 2, hi = (q + 1) / S + 2;
+    for (int p = lo; p <= hi; ++p) {
+        if (p < 0 || p >= n_out) continue;
+        for (int t = 0; t < 3; ++t) {
+            int i = S * p + t - 1;
+            i = i < 0 ? -i : i;
+            i = i >= n_in ? 2 * n_in - 2 - i : i;
+            if (i == q && k < 6) {
+                P[k] = p;
+                T[k] = t;
+                ++k;
+            }
+        }
+    }
+    return k;
+}
+
+__global__ __launch_bounds__(256) void dgrad_small_kernel(const DgradSmallArgs a) {
+    const long total = (long)a.B * a.Hin * a.Win * a.Cin;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int ci = (int)(idx % a.Cin);
+    const long pix = idx / a.Cin;
+    const int x = (int)(pix % a.Win);
+    const int y = (int)((pix / a.Win) % a.Hin);
+    const int b = (int)(pix / ((long)a.Win * a.Hin));
+    int Py[6], Ty[6], Px[6], Tx[6];
+    const int ny = refl_taps(y, a.Hin, a.Hout, a.S, Py, Ty);
+    const int nx = refl_taps(x, a.Win, a.Wout, a.S, Px, Tx);
+    float s = 0.0f;
+    for (int i = 0; i < ny; ++i)
+        for (int j = 0; j < nx; ++j) {
+            const float *g = a.G + (((size_t)b * a.Hout + Py[i]) * a.Wout + Px[j]) * a.Gc + a.Goff;
+            const int t = Ty[i] * 3 + Tx[j];
+            for (int co = 0; co < a.Cout; ++co) s = fmaf(g[co], a.W[((size_t)co * a.Cin + ci) * 9 + t], s);
+        }
+    const size_t o = a.Xc ? (size_t)pix * a.Xc + a.Xoff + ci : (size_t)pix;
+    if (a.accumulate) s += a.dX[o];
+    if (a.mask && !(a.mask[o] > 0.0f)) s = 0.0f;
+    a.dX[o] = s;
+}
+
+// --------------------------------------------------------------------------------------------
+// elementwise backward tails
+// --------------------------------------------------------------------------------------------
+// rec = sigmoid(pre): g_pre = g_rec * rec * (1 - rec)
+__global__ void sigmoid_bwd_kernel(const float *g, const float *y, float *out, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) out[i] = g[i] * y[i] * (1.0f - y[i]);
+}
+
+// ConvLSTM cell backward (reference base_layers.py:112-128), per (pixel, channel):
+// gates saved post-activation [i | r | o | g] (4C, original order); gh, gc: grads of h, c
+// (gc may be NULL); c_prev may be NULL (zeros).  Writes G (4C, pre-activation grads, original
+// order) and g_c_prev (C; skipped when NULL).
+__global__ void lstm_bwd_kernel(const float *gates, const float *c, const float *c_prev,
+                                const float *gh, const float *gc, float *G, float *gcp, long npix,
+                                int C) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= npix * C) return;
+    const long p = idx / C;
+    const int ch = (int)(idx % C);
+    const float *gt = gates + p * 4 * C;
+    const float i = gt[ch], r = gt[C + ch], o = gt[2 * C + ch], g = gt[3 * C + ch];
+    const float cc = c[idx];
+    const float cp = c_prev ? c_prev[idx] : 0.0f;
+    const float th = tanhf(cc);
+    const float dh = gh ? gh[idx] : 0.0f;
+    const float dc = (gc ? gc[idx] : 0.0f) + dh * o * (1.0f - th * th);
+    float *Gp = G + p * 4 * C;
+    Gp[ch] = dc * g * i * (1.0f - i);
+    Gp[C + ch] = dc * cp * r * (1.0f - r);
+    Gp[2 * C + ch] = dh * th * o * (1.0f - o);
+    Gp[3 * C + ch] = dc * i * (1.0f - g * g);
+    if (gcp) gcp[idx] = dc * r;
+}
+
+// softshrink backward (reference base_layers.py:11-12): z = relu(v-l) - relu(-v-l)
+// gv = gz * ([v > l] + [v < -l]);  dl_partial[block][c] = sum gz * (-[v > l] + [v < -l]).
+// Thread -> (pixel, channel) with a grid stride that is a multiple of C (fixed channel per
+// thread; requires 256 % C == 0), coalesced over channels.
+__global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, const float *v,
+                                                             const float *lam, float *gv,
+                                                             float *dl_partial, long npix, int C) {
+    __shared__ float red[256];
+    const int c = threadIdx.x % C;
+    const float l = lam[c];
+    const long total = npix * C;
+    float acc = 0.0f;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const float vv = v[i], g = gz[i];
+        const bool up = vv > l, dn = vv < -l;
+        gv[i] = g * ((up ? 1.0f : 0.0f) + (dn ? 1.0f : 0.0f));
+        acc += g * ((dn ? 1.0f : 0.0f) - (up ? 1.0f : 0.0f));
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < C) {
+        float s = 0.0f;
+        for (int k = threadIdx.x; k < 256; k += C) s += red[k];
+        dl_partial[(size_t)blockIdx.x * C + threadIdx.x] = s;
+    }
+}
+
+// dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel
+__global__ void lambda_grad_kernel(const float *dlp, int nbl, int C, float *dst, int accumulate) {
+    for (int c = threadIdx.x; c < C; c += blockDim.x) {
+        float s = 0.0f;
+        for (int b = 0; b < nbl; ++b) s += dlp[(size_t)b * C + c];
+        dst[c] = (accumulate ? dst[c] : 0.0f) + s;
+    }
+}
+
+// z = softshrink(v, lambda) (recompute of the ISTA iterate for the D wgrad)
+__global__ void softshrink_fwd_kernel(const float *v, const float *lam, float *z, long npix, int C) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= npix * C) return;
+    const float x = v[i], l = lam[i % C];
+    z[i] = fmaxf(x - l, 0.0f) - fmaxf(-x - l, 0.0f);
+}
+
+// ConvLSTC cell backward (reference base_layers.py:52-71), per (pixel, channel), Cz = 2C:
+// saved i, f (post-sigmoid, Cz each), o (Cz), z0, c (cell), c_prev (nullable);
+// gz: grad of the LSTC output z (= ISTA z_0); gcl: grad of c (from the next frame, nullable).
+// Writes Gg (2*Cz: [gi | gf] pre-activation), Go (Cz), gz0 (Cz, cell part: = dc * i),
+// gcp (Cz, nullable).
+__global__ void lstc_bwd_kernel(const float *gi_, const float *gf_, const float *go_, const float *z0,
+                                const float *c, const float *c_prev, const float *gz, const float *gcl,
+                                float *Gg, float *Go, float *gz0, float *gcp, long npix, int Cz) {
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= npix * Cz) return;
+    const long p = idx / Cz;
+    const int ch = (int)(idx % Cz);
+    const float i = gi_[idx], f = gf_[idx], o = go_[idx];
+    const float cc = c[idx], th = tanhf(cc);
+    const float cp = c_prev ? c_prev[idx] : 0.0f;
+    const float dz = gz[idx];
+    const float dc = (gcl ? gcl[idx] : 0.0f) + dz * o * (1.0f - th * th);
+    Go[idx] = dz * th * o * (1.0f - o);
+    Gg[p * 2 * Cz + ch] = dc * z0[idx] * i * (1.0f - i);
+    Gg[p * 2 * Cz + Cz + ch] = dc * cp * f * (1.0f - f);
+    gz0[idx] = dc * i;
+    if (gcp) gcp[idx] = dc * f;
+}
+
+// bilinear x2 (align_corners=False) backward: gh[b,y,x,c] (+)= sum over up-pixels (Y, X) of
+// gup[b,Y,X,c] * wy(Y->y) * wx(X->x), with the forward's weights (reference base_layers.py:198)
+__device__ __forceinline__ int up_weights(int y, int n, float (&w)[6], int (&Y)[6]) {
+    int k = 0;
+    for (int yy = 2 * y - 2; yy <= 2 * y + 3; ++yy) {
+        if (yy < 0 || yy >= 2 * n) continue;
+        const float sy = fmaxf(((float)yy + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const int y0 = (int)sy;
+        const int y1 = y0 + (y0 < n - 1 ? 1 : 0);
+        const float l1 = sy - (float)y0, l0 = 1.0f - l1;
+        float wt = 0.0f;
+        if (y0 == y) wt += l0;
+        if (y1 == y) wt += l1;
+        if (wt != 0.0f && k < 6) {
+            w[k] = wt;
+            Y[k] = yy;
+            ++k;
+        }
+    }
+    return k;
+}
+
+__global__ void upsample_bwd_kernel(const float *gup, float *gh, int B, int h, int w, int C,
+                                    int accumulate) {
+    const long total = (long)B * h * w * C;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int c = (int)(idx % C);
+    const long pix = idx / C;
+    const int x = (int)(pix % w);
+    const int y = (int)((pix / w) % h);
+    const int b = (int)(pix / ((long)w * h));
+    float wy[6], wx[6];
+    int Ys[6], Xs[6];
+    const int ny = up_weights(y, h, wy, Ys), nx = up_weights(x, w, wx, Xs);
+    float s = 0.0f;
+    for (int i = 0; i < ny; ++i) {
+        const float *row = gup + (((size_t)b * 2 * h + Ys[i]) * 2 * w) * C + c;
+        float sr = 0.0f;
+        for (int j = 0; j < nx; ++j) sr += row[(size_t)Xs[j] * C] * wx[j];
+        s += sr * wy[i];
+    }
+    gh[idx] = (accumulate ? gh[idx] : 0.0f) + s;
+}
+
+// a = a * (b > 0)   (ReLU mask, elementwise, n floats)
+__global__ void relu_mask_kernel(float *a, const float *b, long n) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n && !(b[i] > 0.0f)) a[i] = 0.0f;
+}
+
+}  // namespace cista

@@ -32,7 +32,8 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2 };
+// STAGE_ZP2: dgrad correlation -- zero padding of 2, output on the padded input domain (H+2)
+enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2, STAGE_ZP2 = 3 };
 enum Epi {
     EPI_BIAS = 0,        // out = acc + b
     EPI_RELU = 1,        // out = relu(acc + b)
@@ -63,6 +64,12 @@ struct ConvArgs {
     const float *aux0;   // epilogue input 0 (x1 / z_old / c_prev / c)
     const float *aux1;   // epilogue input 1 (z0)
     const float *lambda; // EPI_ISTA_P: per-channel threshold
+    // training forward (saved for the BPTT backward; NULL at inference):
+    //   EPI_LSTC_CELL: out1 = sigmoid(i), out2 = sigmoid(f); EPI_LSTC_OUT: out1 = sigmoid(o);
+    //   EPI_ISTA_P: out1 = v (pre-softshrink); EPI_LSTM: out2 = (i, r, o, g) post-activation,
+    //   4*Cout channels in the reference gate order; EPI_UP_Q: out1 = u = relu(acc + b)
+    float *out2;
+    const float *ascale; // optional [2]: {s, 1/s} power-of-two input pre-scale (dgrad inputs)
 };
 
 __device__ __forceinline__ int reflect_clamp(int i, int n) {
@@ -137,6 +144,20 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
         }
         v0 = make_float4(r[0], r[1], r[2], r[3]);
         v1 = make_float4(r[4], r[5], r[6], r[7]);
+    } else if constexpr (STAGE == STAGE_ZP2) {
+        const int iy = iy0 + hy, ix = ix0 + hx;
+        if (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) {
+            v0 = v1 = make_float4(0.f, 0.f, 0.f, 0.f);
+        } else {
+            const float *p = seg + (((size_t)b * a.Hin + iy) * a.Win + ix) * segC + choff + g * 8;
+            v0 = *(const float4 *)p;
+            v1 = *(const float4 *)(p + 4);
+        }
+        if (a.ascale) {
+            const float s = a.ascale[0];
+            v0.x *= s; v0.y *= s; v0.z *= s; v0.w *= s;
+            v1.x *= s; v1.y *= s; v1.z *= s; v1.w *= s;
+        }
     } else {
         const int iy = reflect_clamp(iy0 + hy, a.Hin);
         const int ix = reflect_clamp(ix0 + hx, a.Win);
@@ -269,7 +290,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     const int HWd = (a.TW - 1) * S + 3;
     const int HH = (a.TH - 1) * S + 3;
     const int HPpad = (HH * HWd + 15) & ~15;
-    const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
+    const int iy0 = STAGE == STAGE_ZP2 ? oy0 - 2 : oy0 * S - 1;
+    const int ix0 = STAGE == STAGE_ZP2 ? ox0 - 2 : ox0 * S - 1;
     const int Hsrc = (STAGE == STAGE_UP) ? 2 * a.Hin : a.Hin;
     (void)Hsrc;
 
@@ -413,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     // ---------------------------------- epilogue ----------------------------------------
     // acc[m][n][j]: pixel row (wm*MT_W+m)*16 + 4*(lane>>4) + j, packed column (nt0+n)*16 + lane&15
     const int col = lane & 15;
-    const float ws = *a.wscale;
+    const float ws = *a.wscale * (a.ascale ? a.ascale[1] : 1.0f);
 #pragma unroll
     for (int m = 0; m < MT_W; ++m)
 #pragma unroll
@@ -438,6 +460,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float u = fmaxf(acc[m][n][j] + bz[n], 0.0f);
+                    if (a.out1) {   // training: keep u for the final_conv / ReLU backward
+                        const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
+                        const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
+                        if (p < npix && oy0 + py < a.Hout && ox0 + px < a.Wout)
+                            a.out1[(((size_t)b * a.Hout + oy0 + py) * a.Wout + ox0 + px) * a.Cout +
+                                   (nt0 + n) * 16 + col] = u;
+                    }
 #pragma unroll
                     for (int t = 0; t < 9; ++t) v[t * 4 + j] = fmaf(u, wf[t * a.Cout], v[t * 4 + j]);
                 }
@@ -527,33 +556,59 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const float x = vv[e] + zz[e];
+                            r1[e] = x;
                             r[e] = fmaxf(x - ll[e], 0.0f) - fmaxf(-x - ll[e], 0.0f);
                         }
+                        if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_OUT) {
                         const float4 c = *(const float4 *)(a.aux0 + o);
                         const float *cc = reinterpret_cast<const float *>(&c);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) r[e] = sigmoidf_(vv[e]) * tanhf(cc[e]);
+                        for (int e = 0; e < 4; ++e) {
+                            r1[e] = sigmoidf_(vv[e]);
+                            r[e] = r1[e] * tanhf(cc[e]);
+                        }
+                        if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_CELL) {
                         // packed n-tile order per channel block: (in, forget)
                         const float4 z0 = *(const float4 *)(a.aux1 + o);
                         const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
                         const float *zz = reinterpret_cast<const float *>(&z0);
                         const float *pp = reinterpret_cast<const float *>(&cp);
+                        float si[4], sf[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e)
-                            r[e] = sigmoidf_(vv[4 + e]) * pp[e] + sigmoidf_(vv[e]) * zz[e];
+                        for (int e = 0; e < 4; ++e) {
+                            si[e] = sigmoidf_(vv[e]);
+                            sf[e] = sigmoidf_(vv[4 + e]);
+                            r[e] = sf[e] * pp[e] + si[e] * zz[e];
+                        }
+                        if (a.out1) {
+                            *(float4 *)(a.out1 + o) = make_float4(si[0], si[1], si[2], si[3]);
+                            *(float4 *)(a.out2 + o) = make_float4(sf[0], sf[1], sf[2], sf[3]);
+                        }
                     } else if constexpr (EPI == EPI_LSTM) {
                         // packed n-tile order per channel block: (in, remember, out, cell)
                         const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
                         const float *pp = reinterpret_cast<const float *>(&cp);
+                        float gi[4], gr[4], go[4], gg[4];
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
-                            const float c = sigmoidf_(vv[4 + e]) * pp[e] + sigmoidf_(vv[e]) * tanhf(vv[12 + e]);
+                            gi[e] = sigmoidf_(vv[e]);
+                            gr[e] = sigmoidf_(vv[4 + e]);
+                            go[e] = sigmoidf_(vv[8 + e]);
+                            gg[e] = tanhf(vv[12 + e]);
+                            const float c = gr[e] * pp[e] + gi[e] * gg[e];
                             r1[e] = c;
-                            r[e] = sigmoidf_(vv[8 + e]) * tanhf(c);
+                            r[e] = go[e] * tanhf(c);
                         }
                         *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+                        if (a.out2) {
+                            float *gsv = a.out2 + pix * 4 * a.Cout + ch;
+                            *(float4 *)(gsv) = make_float4(gi[0], gi[1], gi[2], gi[3]);
+                            *(float4 *)(gsv + a.Cout) = make_float4(gr[0], gr[1], gr[2], gr[3]);
+                            *(float4 *)(gsv + 2 * a.Cout) = make_float4(go[0], go[1], go[2], go[3]);
+                            *(float4 *)(gsv + 3 * a.Cout) = make_float4(gg[0], gg[1], gg[2], gg[3]);
+                        }
                     }
                     *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
                 }

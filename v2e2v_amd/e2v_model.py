@@ -11,7 +11,7 @@ Differences a caller can observe (all documented in DESIGN.md):
   any layout are accepted back;
 * the path runs on ROCm devices only; CPU tensors raise (the CPU restatement lives in
   ``oracle/`` and is test infrastructure, never a fallback);
-* numerics: convolutions use the split-bf16 3-pass MFMA scheme (fp32 accumulate); results
+* numerics: convolutions use the split-fp16 3-pass MFMA scheme (fp32 accumulate); results
   match the reference fp32 CPU path within 1e-4 (tests/test_gpu_parity.py).
 """
 from __future__ import annotations
@@ -69,7 +69,7 @@ class CistaLSTCNet(nn.Module):
         ]
 
     def packed_params(self):
-        """Split-bf16 MFMA tiles of the current parameters; repacked whenever any parameter
+        """Split-fp16 MFMA tiles of the current parameters; repacked whenever any parameter
         changed (load_state_dict, optimizer step: tracked through tensor versions)."""
         params = self._unique_params()
         dev = params[0].device
@@ -103,10 +103,19 @@ class CistaLSTCNet(nn.Module):
         """reference e2v/e2v_model.py:41-90.  events (B,nb,H,W), prev_image (B,1,H,W),
         prev_states None or [c_lstc, z, (h, c)] -> (rec_I (B,1,H,W), [c_lstc, z, (h, c)])."""
         if torch.is_grad_enabled() and (events.requires_grad or prev_image.requires_grad or
-                                        any(p.requires_grad for p in self.parameters())):
-            raise RuntimeError("CistaLSTCNet (MI355X build): the BPTT backward kernels are not "
-                               "built yet -- run inference under torch.no_grad()")
+                                        any(p.requires_grad for p in self.parameters()) or
+                                        _states_require_grad(prev_states)):
+            return _train_frame(self, events, prev_image, prev_states)
         return _forward_frame(self, events, prev_image, prev_states)
+
+    def train_workspace(self, B, H, W, device):
+        L = _lib.lib()
+        n = L.cista_train_workspace_bytes(ctypes_ref(self._cfg()), B, H, W)
+        ws = getattr(self, "_tws", None)
+        if ws is None or ws.numel() < n or ws.device != device:
+            ws = torch.empty(n, dtype=torch.uint8, device=device)
+            self._tws = ws
+        return ws
 
 
 def ctypes_ref(x):
@@ -170,4 +179,113 @@ def _forward_frame(model, events, prev_image, prev_states):
     _lib.check(L.cista_forward(ctypes_ref(model._cfg()), packed.data_ptr(), B, H, W,
                                ctypes_ref(io), ws.data_ptr(), ws.numel(),
                                _lib.stream_handle(dev)), "cista_forward")
+    return rec, [c_lstc, z, (hs, cs)]
+
+
+# ------------------------------------------------------------------------------------------
+# training: one autograd node per frame (BPTT through prev_image and the states is autograd's
+# own chaining across frames, like the reference train_e2v.py:108-130)
+# ------------------------------------------------------------------------------------------
+def _states_require_grad(prev_states):
+    if prev_states is None:
+        return False
+    flat = [prev_states[0], prev_states[-2]] + (list(prev_states[-1]) if prev_states[-1] is not None else [])
+    return any(t is not None and t.requires_grad for t in flat)
+
+
+def _cl(t):
+    return None if t is None else t.detach().float().contiguous(memory_format=torch.channels_last)
+
+
+class _CistaFrame(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, model, events, prev_image, c_lstc_p, z_p, h_p, c_p, *params):
+        packed = model.packed_params()
+        dev = packed.device
+        B, nb, H, W = events.shape
+        C = model.base_channels
+        h, w = H // 2, W // 2
+        cl = torch.channels_last
+        ev = events.detach().float().contiguous()
+        pi = prev_image.detach().float().contiguous()
+        c_lstc_p, z_p, h_p, c_p = _cl(c_lstc_p), _cl(z_p), _cl(h_p), _cl(c_p)
+        rec = torch.empty(B, 1, H, W, device=dev)
+        c_lstc = torch.empty(B, 2 * C, h, w, device=dev, memory_format=cl)
+        z = torch.empty(B, 2 * C, h, w, device=dev, memory_format=cl)
+        hs = torch.empty(B, C, h, w, device=dev, memory_format=cl)
+        cs = torch.empty(B, C, h, w, device=dev, memory_format=cl)
+        L = _lib.lib()
+        cfg = model._cfg()
+        saved = torch.empty(L.cista_saved_bytes(ctypes_ref(cfg), B, H, W), dtype=torch.uint8, device=dev)
+        ws = model.train_workspace(B, H, W, dev)
+        P = _lib.ptr
+        io = _lib.CistaFrameIO(P(ev), P(pi), P(c_lstc_p), P(z_p), P(h_p), P(c_p),
+                               P(rec), P(c_lstc), P(z), P(hs), P(cs))
+        _lib.check(L.cista_forward_train(ctypes_ref(cfg), packed.data_ptr(), B, H, W, ctypes_ref(io),
+                                         saved.data_ptr(), saved.numel(), ws.data_ptr(), ws.numel(),
+                                         _lib.stream_handle(dev)), "cista_forward_train")
+        ctx.model = model
+        ctx.has = [t is not None for t in (c_lstc_p, z_p, h_p, c_p)]
+        ctx.save_for_backward(ev, pi, *[t if t is not None else torch.empty(0) for t in (c_lstc_p, z_p, h_p, c_p)],
+                              rec, c_lstc, z, hs, cs, saved)
+        return rec, c_lstc, z, hs, cs
+
+    @staticmethod
+    def backward(ctx, g_rec, g_cl, g_z, g_h, g_c):
+        model = ctx.model
+        ev, pi, clp, zp, hp, cp, rec, c_lstc, z, hs, cs, saved = ctx.saved_tensors
+        clp, zp, hp, cp = [t if has else None for t, has in zip((clp, zp, hp, cp), ctx.has)]
+        dev = rec.device
+        B, _, H, W = rec.shape
+        L = _lib.lib()
+        cfg = model._cfg()
+        params = [p.detach().float().contiguous() for p in model._unique_params()]
+        g_rec = None if g_rec is None else g_rec.float().contiguous()
+        g_cl, g_z, g_h, g_c = _cl(g_cl), _cl(g_z), _cl(g_h), _cl(g_c)
+        need = ctx.needs_input_grad
+        g_pi = torch.empty_like(pi) if need[2] else None
+        g_clp = torch.empty_like(clp, memory_format=torch.channels_last) if (clp is not None and need[3]) else None
+        g_zp = torch.empty_like(zp, memory_format=torch.channels_last) if (zp is not None and need[4]) else None
+        g_hp = torch.empty_like(hp, memory_format=torch.channels_last) if (hp is not None and need[5]) else None
+        g_cp = torch.empty_like(cp, memory_format=torch.channels_last) if (cp is not None and need[6]) else None
+        pgrads = [torch.empty_like(p) for p in params]
+        P = _lib.ptr
+        io = _lib.CistaFrameIO(P(ev), P(pi), P(clp), P(zp), P(hp), P(cp), P(rec), P(c_lstc), P(z), P(hs), P(cs))
+        gio = _lib.CistaGradIO(P(g_rec), P(g_cl), P(g_z), P(g_h), P(g_c), P(g_pi), P(g_clp), P(g_zp),
+                               P(g_hp), P(g_cp))
+        cp_ = _lib.CistaParams(*[t.data_ptr() for t in params])
+        pg = _lib.CistaParamGrads(*[t.data_ptr() for t in pgrads])
+        ws = model.train_workspace(B, H, W, dev)
+        _lib.check(L.cista_backward(ctypes_ref(cfg), model.packed_params().data_ptr(), ctypes_ref(cp_),
+                                    B, H, W, ctypes_ref(io), saved.data_ptr(), saved.numel(),
+                                    ctypes_ref(gio), ctypes_ref(pg), ws.data_ptr(), ws.numel(),
+                                    _lib.stream_handle(dev)), "cista_backward")
+        # keep the host-side argument tensors alive until the stream has consumed them
+        model._bwd_keepalive = (params, g_rec, g_cl, g_z, g_h, g_c)
+        return (None, None, g_pi, g_clp, g_zp, g_hp, g_cp, *pgrads)
+
+
+def _train_frame(model, events, prev_image, prev_states):
+    packed = model.packed_params()
+    dev = packed.device
+    if events.dim() != 4 or events.shape[1] != model.num_bins:
+        raise RuntimeError(f"events must be (B, {model.num_bins}, H, W), got {tuple(events.shape)}")
+    B, nb, H, W = events.shape
+    C = model.base_channels
+    if H % 2 or W % 2:
+        raise RuntimeError(f"H and W must be even (reference upsampling needs it), got {H}x{W}")
+    _check_input("events", events, (B, nb, H, W), dev)
+    _check_input("prev_image", prev_image, (B, 1, H, W), dev)
+    h, w = H // 2, W // 2
+    if prev_states is None:
+        prev_states = [None] * model.num_states
+    hc = prev_states[-1]
+    sts = [prev_states[0], prev_states[-2], None if hc is None else hc[0], None if hc is None else hc[1]]
+    shapes = [(B, 2 * C, h, w), (B, 2 * C, h, w), (B, C, h, w), (B, C, h, w)]
+    for i, (t, shp) in enumerate(zip(sts, shapes)):
+        if t is not None:
+            _check_input(f"prev_states[{i}]", t, shp, dev)
+    if (sts[2] is None) != (sts[3] is None):
+        raise RuntimeError("prev_states[2] must be None or an (h, c) pair")
+    rec, c_lstc, z, hs, cs = _CistaFrame.apply(model, events, prev_image, *sts, *model._unique_params())
     return rec, [c_lstc, z, (hs, cs)]
