@@ -51,7 +51,71 @@ def parse():
                    help="frames of the bounded CPU-baseline sample (one sequence, B=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--layer-reps", type=int, default=10)
-    return p.parse_args()
+    p.add_argument("--mode", choices=["infer", "train"], default="infer",
+                   help="infer: the headline metric (config c2); train: BPTT step (configs c3/c4)")
+    args = p.parse_args()
+    if args.mode == "train" and "--batch" not in sys.argv:
+        args.batch = 8            # BASELINE config c3: batch 8 per GPU (c4: 8 GPUs x 8 = 64)
+    return args
+
+
+def train_main(args, torch, vd, rank, world, device):
+    """BPTT training step of train_e2v.py:108-130 on the HIP path: len_sequence frames with
+    prev_img = output.clone() (no detach) and states carried, loss on the last frame, one
+    backward through the whole sequence, Adam step.  Loss = L1 (the reference adds LPIPS-VGG,
+    whose weights need a network download, and 1-SSIM: SURVEY 8 row f3, not built).  Multi-GPU:
+    DistributedDataParallel over RCCL (one gradient all-reduce per step)."""
+    from v2e2v_amd import CistaLSTCNet
+    B, L, H, W = args.batch, args.len_seq, args.height, args.width
+    model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
+    he_init_(torch, model, seed=7)
+    model = model.to(device).train()
+    net = model
+    if world > 1:
+        net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index],
+                                                        broadcast_buffers=False)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    vox = synth_voxels(torch, L, B, 5, H, W, args.num_events, seed=2000 + rank, device=device)
+    target = torch.rand(B, 1, H, W, device=device, generator=torch.Generator(device=device).manual_seed(3))
+
+    def step():
+        prev = torch.zeros(B, 1, H, W, device=device)
+        state = None
+        for s in range(L):
+            out, state = net(vox[s], prev, state)
+            prev = out.clone()
+        loss = torch.nn.functional.l1_loss(out, target)
+        opt.zero_grad(set_to_none=True)
+        loss.backward()
+        opt.step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    vd.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        loss = step()
+    torch.cuda.synchronize()
+    vd.barrier()
+    elapsed = vd.max_over_ranks(time.perf_counter() - t0, device)
+    frames = world * B * L * args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "BPTT training frames/sec at 180x240 5-bin depth=5 (len_sequence 15)",
+            "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic (GPU-generated 15000-event voxels, random targets; L1 loss)",
+            "config": {"workload": f"train_e2v BPTT len {L}, batch {B}/GPU, {H}x{W}",
+                       "batch_per_gpu": B, "global_batch": B * world, "len_sequence": L,
+                       "parallelism": f"ddp{world}" if world > 1 else "single"},
+            "loss": float(loss.item()),
+            "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 # ------------------------------------------------------------------ synthetic inputs (GPU)
@@ -206,6 +270,8 @@ def main():
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     vd.init("nccl", device)
+    if args.mode == "train":
+        return train_main(args, torch, vd, rank, world, device)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
 
     model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
