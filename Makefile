@@ -6,7 +6,7 @@ HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
 
 LIB  = v2e2v_amd/libcista_hip.so
 SRCS = v2e2v_amd/csrc/cista_abi.hip
-DEPS = $(SRCS) v2e2v_amd/csrc/cista_kernels.hpp include/cista_lstc.h
+DEPS = $(SRCS) v2e2v_amd/csrc/cista_kernels.hpp v2e2v_amd/csrc/cista_backward.hpp include/cista_lstc.h
 
 all: $(LIB)
 

@@ -19,6 +19,16 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.err; [ $rc -eq 0 ] || exit $rc ;;
+    ttests)
+      timeout -k 10 600 python -m pytest tests/test_gpu_train.py -m gpu -q -p no:cacheprovider > gpurun_out/gpu_ttests.log 2>&1
+      rc=$?; echo "ttests rc=$rc"; tail -12 gpurun_out/gpu_ttests.log; ok $rc || exit $rc ;;
+    tbench)
+      timeout -k 10 600 python bench.py --mode train ${TBENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/tbench.json 2> gpurun_out/tbench.err
+      rc=$?; echo "tbench rc=$rc"; cat gpurun_out/tbench.json; tail -3 gpurun_out/tbench.err; [ $rc -eq 0 ] || exit $rc ;;
+    tprof)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/proft -o run -- python3 bench.py --mode train --steps 1 --warmup 1 > gpurun_out/proft_bench.json 2> gpurun_out/proft.err
+      rc=$?; echo "tprof rc=$rc"; tail -3 gpurun_out/proft.err; [ $rc -eq 0 ] || exit $rc ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; echo "list rc=$?" ;;
     sq)

@@ -482,11 +482,12 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
     return s;
 }
 
-constexpr int WG_SPLIT_MAX = 64;
+constexpr int WG_BLOCKS = 1024;          // wgrad workgroups per launch (splits x cout/cin blocks)
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
-    float *part, *dlp;
+    float *part, *bpart, *dlp;
+    float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
     unsigned *amax;     // [8] absmax bits
     float *scl;         // [16] scale pairs
     size_t bytes;
@@ -517,8 +518,10 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.gx1 = take(hw * C);
     s.Go = take(hw * 2 * C);
     s.gz0 = take(hw * 2 * C);
-    s.part = take((size_t)WG_SPLIT_MAX * (4 * C) * (4 * C) * 9);
+    s.part = take((size_t)WG_BLOCKS * 32 * 32 * 9);
+    s.bpart = take((size_t)WG_BLOCKS * 4 * C);
     s.dlp = take((size_t)2 * C * 512);
+    s.wT = take((size_t)9 * C * C);
     s.amax = reinterpret_cast<unsigned *>(take(16));
     s.scl = take(32);
     s.bytes = off;
@@ -564,11 +567,12 @@ struct Bwd {
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
 
-// dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor
+// dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor; and, when
+// db != NULL, db (+)= sign * (pixel sum of G) from the same pass over G (bias gradient)
 template <int XS>
 int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, int x0c,
           const float *X1, int x1c, int Cin, int Hin, int Win, int Hout, int Wout, float *dst,
-          float sign, int accumulate) {
+          float sign, int accumulate, float *db) {
     WgradArgs a;
     memset(&a, 0, sizeof(a));
     a.G = G; a.Gc = Gc; a.Goff = Goff;
@@ -582,12 +586,14 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     a.Cout = Cout; a.Cin = Cin;
     const int nblk = ((Cout + 31) / 32) * ((Cin + 31) / 32);
     const int ntiles = k.B * a.tiles_y * a.tiles_x;
-    int ns = (2048 + nblk - 1) / nblk;
-    ns = ns > WG_SPLIT_MAX ? WG_SPLIT_MAX : ns;
+    int ns = WG_BLOCKS / nblk;
     ns = ns > ntiles ? ntiles : ns;
     ns = ns < 1 ? 1 : ns;
+    ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
     a.nsplit = ns;
     a.partial = k.ws.part;
+    a.bpartial = db ? k.ws.bpart : nullptr;
+    a.vec4 = XS != XS_NCHW && Gc % 4 == 0 && Goff % 4 == 0 && x0c % 4 == 0 && x1c % 4 == 0 && Cin % 4 == 0;
     constexpr int S = XS == XS_S2 ? 2 : 1;
     const int HP = ((a.TH - 1) * S + 3) * ((a.TW - 1) * S + 3);
     const size_t lds = ((size_t)((a.TH * a.TW + 3) & ~3) + HP) * 33 * 4;
@@ -597,17 +603,19 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     const long n = (long)Cout * Cin * 9;
     hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
                        dst, sign, accumulate);
+    if (db)
+        hipLaunchKernelGGL(reduce_partials_kernel, g1d(Cout), dim3(256), 0, k.st, (const float *)k.ws.bpart, ns,
+                           (long)Cout, db, sign, accumulate);
     return hip_ok();
 }
 
-int bias_grad(Bwd &k, const float *G, int Gc, int Goff, int n, long npix, float *dst, float sign,
-              int accumulate) {
-    int ns = (int)((npix + 4095) / 4096);
-    ns = ns < 1 ? 1 : (ns > 256 ? 256 : ns);
-    hipLaunchKernelGGL(channel_sum_kernel, dim3((n + 63) / 64, ns), dim3(256), 0, k.st, G, Gc, Goff, n, npix,
-                       k.ws.part);
-    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, (long)n,
-                       dst, sign, accumulate);
+// VALU dgrad through a reference-layout weight (W0: stride 2; final conv: Cout 1)
+int dgrad_vec(Bwd &k, const DgradSmallArgs &d, const float *Wref) {
+    if (d.Cin % 4 || d.Xc % 4 || d.Xoff % 4 || (size_t)d.Cout * d.Cin > (size_t)k.C * k.C) return CISTA_ERR_UNSUPPORTED;
+    hipLaunchKernelGGL(transpose_w_kernel, g1d((long)d.Cout * d.Cin * 9), dim3(256), 0, k.st, Wref, d.Cout, d.Cin,
+                       k.ws.wT);
+    hipLaunchKernelGGL(dgrad_vec_kernel, g1d((long)d.B * d.Hin * d.Win * (d.Cin / 4)), dim3(256), 0, k.st, d,
+                       (const float *)k.ws.wT);
     return hip_ok();
 }
 
@@ -660,15 +668,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
     if (g.g_rec) {
         hipLaunchKernelGGL(sigmoid_bwd_kernel, g1d(HW), dim3(256), 0, st, g.g_rec, io.rec, ws.gpre, HW);
-        CHECK(bias_grad(k, ws.gpre, 1, 0, 1, HW, pg.final_b, 1.0f, 0));
-        CHECK(wgrad<XS_S1>(k, ws.gpre, 1, 0, 1, sv.u, C, nullptr, 0, C, H, W, H, W, pg.final_w, 1.0f, 0));
+        CHECK(wgrad<XS_S1>(k, ws.gpre, 1, 0, 1, sv.u, C, nullptr, 0, C, H, W, H, W, pg.final_w, 1.0f, 0, pg.final_b));
         DgradSmallArgs d;
         d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
         d.mask = sv.u; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = 1; d.Cin = C;
         d.accumulate = 0;
-        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * C), dim3(256), 0, st, d);   // g_U (ReLU'd)
-        CHECK(bias_grad(k, ws.gU, C, 0, C, HW, pg.up_b, 1.0f, 0));
-        CHECK(wgrad<XS_UP>(k, ws.gU, C, 0, C, io.h, C, nullptr, 0, C, h, w, H, W, pg.up_w, 1.0f, 0));
+        CHECK(dgrad_vec(k, d, P.final_w));                                              // g_U (ReLU'd)
+        CHECK(wgrad<XS_UP>(k, ws.gU, C, 0, C, io.h, C, nullptr, 0, C, h, w, H, W, pg.up_w, 1.0f, 0, pg.up_b));
         CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF));
         CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
         hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
@@ -683,14 +689,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     // ---- 3. ConvLSTM ---------------------------------------------------------------------
     hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C);
-    CHECK(bias_grad(k, ws.Gl, 4 * C, 0, 4 * C, hw, pg.lstm_b, 1.0f, 0));
-    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b));
     CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y));        // relu(Dg) mask
     if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
-    CHECK(bias_grad(k, ws.gy, C, 0, C, hw, pg.Dg_b, 1.0f, 0));
-    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b));
     CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp));
     CHECK(copy_or_zero(ws.gz, g.g_z, (size_t)hw * 2 * C, st));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
@@ -719,19 +723,17 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                            lam, ws.gv, ws.dlp, hw, 2 * C);
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
-        CHECK(bias_grad(k, ws.gv, 2 * C, 0, 2 * C, hw, pg.P_b, 1.0f, it != D - 1));
-        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1));
+        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b));
         CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp));
         CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr));
         CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
-        CHECK(bias_grad(k, ws.gxk, C, 0, C, hw, pg.D_b, -1.0f, it != D - 1));
-        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1));
+        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b));
         CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp));
         CHECK(copy_or_zero(ws.gz, ws.gv, (size_t)hw * 2 * C, st));          // identity path
         CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 1, nullptr));
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
-        hipLaunchKernelGGL(lambda_grad_kernel, dim3(1), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
+        hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
                            pg.lambda, it != D - 1);
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------
@@ -740,25 +742,22 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C);
-    CHECK(bias_grad(k, ws.Go, 2 * C, 0, 2 * C, hw, pg.out_gates_b, 1.0f, 0));
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
-                       pg.out_gates_w, 1.0f, 0));
+                       pg.out_gates_w, 1.0f, 0, pg.out_gates_b));
     CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp));
     CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
-    CHECK(bias_grad(k, ws.Gl, 4 * C, 0, 4 * C, hw, pg.gates_b, 1.0f, 0));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
-                       pg.gates_w, 1.0f, 0));
+                       pg.gates_w, 1.0f, 0, pg.gates_b));
     CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp));
     CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
-    CHECK(bias_grad(k, ws.gz0, 2 * C, 0, 2 * C, hw, pg.P0_b, 1.0f, 0));
-    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0));
+    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b));
     CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp));
     CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
-    float *xfull = ws.gU, *gxfull = ws.dxpF;
+    float *xfull = ws.gU, *gxfull = ws.gU;   // x_full is dead once W0's wgrad has run
     {
         Frame f;
         memset(&f, 0, sizeof(f));
@@ -766,20 +765,20 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         f.C = C; f.events = io.events; f.prev_image = io.prev_image; f.full = xfull; f.st = st;
         CHECK(run_layer(f, CISTA_LAYER_INPUT));
     }
-    CHECK(bias_grad(k, ws.gx1, C, 0, C, hw, pg.W0_b, 1.0f, 0));
-    CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0));
+    CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
     {
-        DgradSmallArgs d;
-        d.G = ws.gx1; d.Gc = C; d.Goff = 0; d.W = P.W0_w; d.dX = gxfull; d.Xc = C; d.Xoff = 0; d.mask = nullptr;
-        d.B = B; d.Hin = H; d.Win = W; d.Hout = h; d.Wout = w; d.S = 2; d.Cout = C; d.Cin = C; d.accumulate = 0;
-        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * C), dim3(256), 0, st, d);
+        // padded-domain stride-2 dgrad into dxpF, then reflect-fold into gxfull
+        const int Hp = H + 2, Wp = W + 2, ngx = (((Wp + 1) / 2) + 3) / 4;
+        hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * C * 9), dim3(256), 0, st, P.W0_w, C, C, ws.wT);
+        hipLaunchKernelGGL(dgrad_s2_kernel, g1d((long)B * Hp * 2 * ngx * (C / 4)), dim3(256), 0, st,
+                           (const float *)ws.gx1, C, 0, (const float *)ws.wT, C, C, B, h, w, ws.dxpF, Hp, Wp);
+        CHECK(fold(k, ws.dxpF, C, 0, gxfull, C, 0, C, H, W, 1.0f, 0, nullptr));
     }
     // ---- 8. We / Wi ----------------------------------------------------------------------------
     const int half = C / 2, nb = k.cfg->num_bins;
-    CHECK(bias_grad(k, gxfull, C, 0, half, HW, pg.We_b, 1.0f, 0));
-    CHECK(bias_grad(k, gxfull, C, half, half, HW, pg.Wi_b, 1.0f, 0));
-    CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0));
-    CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0));
+    CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0, pg.We_b));
+    CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0,
+                         pg.Wi_b));
     if (g.g_prev_image) {
         DgradSmallArgs d;
         d.G = gxfull; d.Gc = C; d.Goff = half; d.W = P.Wi_w; d.dX = g.g_prev_image; d.Xc = 0; d.Xoff = 0;

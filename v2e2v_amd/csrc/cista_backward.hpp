@@ -121,6 +121,10 @@ struct WgradArgs {
     int Cout, Cin;                      // forward conv shape
     int nsplit;
     float *partial;                     // [nsplit][Cout][Cin][9]
+    float *bpartial;                    // optional [nsplit][Cout]: bias grads (pixel sums of G),
+                                        // produced by the ci-block-0 workgroups
+    int vec4;                           // float4 staging: Gc, Goff, x0c, x1c, Cin % 4 == 0, NHWC
+                                        // input, tile <= 16x16 (S1/UP) or 8x8 (S2)
 };
 
 typedef float f32x4w __attribute__((ext_vector_type(4)));
@@ -154,6 +158,44 @@ __device__ __forceinline__ float wg_load_x(const WgradArgs &a, int b, int iy, in
     }
 }
 
+// four consecutive input channels ci..ci+3 (ci % 4 == 0, segment bounds % 4 == 0; NHWC only)
+template <int XS>
+__device__ __forceinline__ float4 wg_load_x4(const WgradArgs &a, int b, int iy, int ix, int ci) {
+    const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (ci >= a.Cin) return z;
+    const bool s0 = ci < a.x0c;
+    const float *seg = s0 ? a.X0 : a.X1;
+    const int segC = s0 ? a.x0c : a.x1c;
+    const int cc = s0 ? ci : ci - a.x0c;
+    if (!seg) return z;
+    if constexpr (XS == XS_UP) {
+        const int Hu = 2 * a.Hin, Wu = 2 * a.Win;
+        const int Y = reflect_clamp(iy, Hu), X = reflect_clamp(ix, Wu);
+        float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
+        float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const int y0 = (int)sy, x0 = (int)sx;
+        const int y1 = y0 + (y0 < a.Hin - 1 ? 1 : 0), x1 = x0 + (x0 < a.Win - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1, lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+        const float *base = seg + (size_t)b * a.Hin * a.Win * segC + cc;
+        const float4 v00 = *reinterpret_cast<const float4 *>(base + ((size_t)y0 * a.Win + x0) * segC);
+        const float4 v01 = *reinterpret_cast<const float4 *>(base + ((size_t)y0 * a.Win + x1) * segC);
+        const float4 v10 = *reinterpret_cast<const float4 *>(base + ((size_t)y1 * a.Win + x0) * segC);
+        const float4 v11 = *reinterpret_cast<const float4 *>(base + ((size_t)y1 * a.Win + x1) * segC);
+        float4 r;
+        r.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
+        r.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
+        r.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
+        r.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+        return r;
+    } else {
+        if constexpr (XS == XS_NCHW)   // never selected on the host (vec4 = 0); plain loads
+            return make_float4(wg_load_x<XS>(a, b, iy, ix, ci), wg_load_x<XS>(a, b, iy, ix, ci + 1),
+                               wg_load_x<XS>(a, b, iy, ix, ci + 2), wg_load_x<XS>(a, b, iy, ix, ci + 3));
+        const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
+        return *reinterpret_cast<const float4 *>(seg + (((size_t)b * a.Hin + y) * a.Win + x) * segC + cc);
+    }
+}
+
 // workgroup: 4 waves = 2 (cout 16-blocks) x 2 (cin 16-blocks); blockIdx.x = (co32, ci32) block,
 // blockIdx.y = split; the split loops over pixel tiles t = split, split + nsplit, ...
 template <int XS>
@@ -174,6 +216,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
     f32x4w acc[9];
 #pragma unroll
     for (int t = 0; t < 9; ++t) acc[t] = f32x4w{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = a.bpartial && (blockIdx.x % nci) == 0;
+    float bsum = 0.0f;                       // thread: channel tid & 31, pixel phase tid >> 5
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
         int tt = tile;
@@ -183,24 +227,86 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
         const int b = tt / a.tiles_y;
         const int oy0 = ty * TH, ox0 = tx * TW;
         __syncthreads();
-        // stage G tile (zero outside the image / beyond Cout)
-        for (int i = threadIdx.x; i < NPX4 * 32; i += 256) {
-            const int p = i >> 5, c = i & 31;
-            const int py = p / TW, px = p - py * TW;
-            const int oy = oy0 + py, ox = ox0 + px;
-            float v = 0.0f;
-            if (p < NPX && oy < a.Hout && ox < a.Wout && co0 + c < a.Cout)
-                v = a.G[(((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + c];
-            Gs[p * 33 + c] = v;
-        }
-        // stage the input halo
+        // stage G tile (zero outside the image / beyond Cout) and the input halo: all of a
+        // thread's global loads are issued before the first LDS store (latency overlap)
         const int iy0 = oy0 * S - 1, ix0 = ox0 * S - 1;
-        for (int i = threadIdx.x; i < HP * 32; i += 256) {
-            const int hp = i >> 5, c = i & 31;
-            const int hy = hp / HWd, hx = hp - hy * HWd;
-            Xs[hp * 33 + c] = wg_load_x<XS>(a, b, iy0 + hy, ix0 + hx, ci0 + c);
+        if (a.vec4) {
+            constexpr int UG = 8, UX = 11;   // 256 px x 8 quads; (17*2+1)^2 or 18^2 halo x 8 quads
+            float4 gv[UG], xv[UX];
+#pragma unroll
+            for (int u = 0; u < UG; ++u) {
+                const int i = threadIdx.x + u * 256;
+                const int p = i >> 3, c = (i & 7) * 4;
+                const int py = p / TW, px = p - py * TW;
+                const int oy = oy0 + py, ox = ox0 + px;
+                gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (p < NPX && oy < a.Hout && ox < a.Wout && co0 + c < a.Cout)
+                    gv[u] = *reinterpret_cast<const float4 *>(
+                        a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + c);
+            }
+#pragma unroll
+            for (int u = 0; u < UX; ++u) {
+                const int i = threadIdx.x + u * 256;
+                const int hp = i >> 3, c = (i & 7) * 4;
+                const int hy = hp / HWd, hx = hp - hy * HWd;
+                xv[u] = hp < HP ? wg_load_x4<XS>(a, b, iy0 + hy, ix0 + hx, ci0 + c) : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
+#pragma unroll
+            for (int u = 0; u < UG; ++u) {
+                const int i = threadIdx.x + u * 256;
+                const int p = i >> 3, c = (i & 7) * 4;
+                if (p < NPX4) {
+                    float *d = Gs + p * 33 + c;
+                    d[0] = gv[u].x; d[1] = gv[u].y; d[2] = gv[u].z; d[3] = gv[u].w;
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < UX; ++u) {
+                const int i = threadIdx.x + u * 256;
+                const int hp = i >> 3, c = (i & 7) * 4;
+                if (hp < HP) {
+                    float *d = Xs + hp * 33 + c;
+                    d[0] = xv[u].x; d[1] = xv[u].y; d[2] = xv[u].z; d[3] = xv[u].w;
+                }
+            }
+        } else {
+            for (int i0 = threadIdx.x; i0 < NPX4 * 32; i0 += 256 * 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256;
+                    const int p = i >> 5, c = i & 31;
+                    const int py = p / TW, px = p - py * TW;
+                    const int oy = oy0 + py, ox = ox0 + px;
+                    v[u] = 0.0f;
+                    if (p < NPX && oy < a.Hout && ox < a.Wout && co0 + c < a.Cout)
+                        v[u] = a.G[(((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + c];
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256;
+                    if (i < NPX4 * 32) Gs[(i >> 5) * 33 + (i & 31)] = v[u];
+                }
+            }
+            for (int i0 = threadIdx.x; i0 < HP * 32; i0 += 256 * 8) {
+                float v[8];
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256;
+                    const int hp = i >> 5, c = i & 31;
+                    const int hy = hp / HWd, hx = hp - hy * HWd;
+                    v[u] = i < HP * 32 ? wg_load_x<XS>(a, b, iy0 + hy, ix0 + hx, ci0 + c) : 0.0f;
+                }
+#pragma unroll
+                for (int u = 0; u < 8; ++u) {
+                    const int i = i0 + u * 256;
+                    if (i < HP * 32) Xs[(i >> 5) * 33 + (i & 31)] = v[u];
+                }
+            }
         }
         __syncthreads();
+        if (do_bias)
+            for (int p = threadIdx.x >> 5; p < NPX4; p += 8) bsum += Gs[p * 33 + (threadIdx.x & 31)];
         for (int p4 = 0; p4 < NPX4; p4 += 4) {
             const int p = p4 + (lane >> 4);
             const float av = Gs[p * 33 + wco + (lane & 15)];
@@ -212,6 +318,17 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
                 const float bv = Xs[(hb + (t / 3) * HWd + (t % 3)) * 33 + wci + (lane & 15)];
                 acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[t], 0, 0, 0);
             }
+        }
+    }
+    if (do_bias) {
+        __syncthreads();
+        Gs[threadIdx.x] = bsum;
+        __syncthreads();
+        if (threadIdx.x < 32) {
+            float t = 0.0f;
+            for (int k = 0; k < 8; ++k) t += Gs[k * 32 + threadIdx.x];
+            if (co0 + (int)threadIdx.x < a.Cout)
+                a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + threadIdx.x] = t;
         }
     }
     // acc[t][j]: row (cout) 4*(lane>>4) + j, col (cin) lane & 15
@@ -231,27 +348,16 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *parti
                                                               float *dst, float sign, int accumulate) {
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    float s = 0.0f;
-    for (int k = 0; k < nsplit; ++k) s += partial[(size_t)k * n + i];
-    dst[i] = (accumulate ? dst[i] : 0.0f) + sign * s;
-}
-
-// per-channel pixel sums, phase 1: grid (ceil(n/64), nsplit); block = 64 channels x 4 pixel
-// rows; partial[split][c] = sum over the split's pixels of G[p][Goff + c]
-__global__ __launch_bounds__(256) void channel_sum_kernel(const float *G, int Gc, int Goff, int n, long npix,
-                                                          float *partial) {
-    __shared__ float red[4][64];
-    const int c = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int r = threadIdx.x >> 6;
-    const long step = (long)gridDim.y * 4;
-    float s = 0.0f;
-    if (c < n)
-        for (long p = (long)blockIdx.y * 4 + r; p < npix; p += step) s += G[(size_t)p * Gc + Goff + c];
-    red[r][threadIdx.x & 63] = s;
-    __syncthreads();
-    if (r == 0 && c < n)
-        partial[(size_t)blockIdx.y * n + c] = red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
-                                              red[3][threadIdx.x];
+    float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+    int k = 0;
+    for (; k + 4 <= nsplit; k += 4) {
+        s0 += partial[(size_t)k * n + i];
+        s1 += partial[(size_t)(k + 1) * n + i];
+        s2 += partial[(size_t)(k + 2) * n + i];
+        s3 += partial[(size_t)(k + 3) * n + i];
+    }
+    for (; k < nsplit; ++k) s0 += partial[(size_t)k * n + i];
+    dst[i] = (accumulate ? dst[i] : 0.0f) + sign * ((s0 + s1) + (s2 + s3));
 }
 
 // --------------------------------------------------------------------------------------------
@@ -306,12 +412,140 @@ __global__ __launch_bounds__(256) void dgrad_small_kernel(const DgradSmallArgs a
         for (int j = 0; j < nx; ++j) {
             const float *g = a.G + (((size_t)b * a.Hout + Py[i]) * a.Wout + Px[j]) * a.Gc + a.Goff;
             const int t = Ty[i] * 3 + Tx[j];
-            for (int co = 0; co < a.Cout; ++co) s = fmaf(g[co], a.W[((size_t)co * a.Cin + ci) * 9 + t], s);
+            if (((a.Cout | a.Gc | a.Goff) & 3) == 0) {      // float4 along Cout
+                for (int co = 0; co < a.Cout; co += 4) {
+                    const float4 gv = *reinterpret_cast<const float4 *>(g + co);
+                    const float *wp = a.W + ((size_t)co * a.Cin + ci) * 9 + t;
+                    const size_t ws = (size_t)a.Cin * 9;
+                    s = fmaf(gv.x, wp[0], fmaf(gv.y, wp[ws], fmaf(gv.z, wp[2 * ws], fmaf(gv.w, wp[3 * ws], s))));
+                }
+            } else {
+                for (int co = 0; co < a.Cout; ++co) s = fmaf(g[co], a.W[((size_t)co * a.Cin + ci) * 9 + t], s);
+            }
         }
     const size_t o = a.Xc ? (size_t)pix * a.Xc + a.Xoff + ci : (size_t)pix;
     if (a.accumulate) s += a.dX[o];
     if (a.mask && !(a.mask[o] > 0.0f)) s = 0.0f;
     a.dX[o] = s;
+}
+
+// W [Cout][Cin][9] -> WT [9][Cout][Cin] (the layout dgrad_vec_kernel reads as float4 along Cin)
+__global__ void transpose_w_kernel(const float *W, int Cout, int Cin, float *WT) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= Cout * Cin * 9) return;
+    const int t = i % 9, ci = (i / 9) % Cin, co = i / (9 * Cin);
+    WT[((size_t)t * Cout + co) * Cin + ci] = W[i];
+}
+
+// dgrad_small_kernel with 4 input channels per thread (Cin % 4 == 0, Xc % 4 == 0): one
+// float4 weight load feeds 4 FMAs, the G value is a wave-uniform-per-pixel broadcast.
+// Used for W0 (stride 2, 64 -> 64) and the final conv (1 -> C, ReLU mask).
+__global__ __launch_bounds__(256) void dgrad_vec_kernel(const DgradSmallArgs a, const float *WT) {
+    const int cq = a.Cin >> 2;
+    const long total = (long)a.B * a.Hin * a.Win * cq;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int ci = (int)(idx % cq) * 4;
+    const long pix = idx / cq;
+    const int x = (int)(pix % a.Win);
+    const int y = (int)((pix / a.Win) % a.Hin);
+    const int b = (int)(pix / ((long)a.Win * a.Hin));
+    int Py[6], Ty[6], Px[6], Tx[6];
+    const int ny = refl_taps(y, a.Hin, a.Hout, a.S, Py, Ty);
+    const int nx = refl_taps(x, a.Win, a.Wout, a.S, Px, Tx);
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < ny; ++i)
+        for (int j = 0; j < nx; ++j) {
+            const float *g = a.G + (((size_t)b * a.Hout + Py[i]) * a.Wout + Px[j]) * a.Gc + a.Goff;
+            const float *w = WT + (size_t)(Ty[i] * 3 + Tx[j]) * a.Cout * a.Cin + ci;
+#pragma unroll 4
+            for (int co = 0; co < a.Cout; ++co) {
+                const float gv = g[co];
+                const float4 wv = *reinterpret_cast<const float4 *>(w + (size_t)co * a.Cin);
+                s.x = fmaf(gv, wv.x, s.x);
+                s.y = fmaf(gv, wv.y, s.y);
+                s.z = fmaf(gv, wv.z, s.z);
+                s.w = fmaf(gv, wv.w, s.w);
+            }
+        }
+    const size_t o = (size_t)pix * a.Xc + a.Xoff + ci;
+    float4 *dst = reinterpret_cast<float4 *>(a.dX + o);
+    if (a.accumulate) {
+        const float4 d = *dst;
+        s.x += d.x; s.y += d.y; s.z += d.z; s.w += d.w;
+    }
+    if (a.mask) {
+        const float4 m = *reinterpret_cast<const float4 *>(a.mask + o);
+        s.x = m.x > 0.0f ? s.x : 0.0f;
+        s.y = m.y > 0.0f ? s.y : 0.0f;
+        s.z = m.z > 0.0f ? s.z : 0.0f;
+        s.w = m.w > 0.0f ? s.w : 0.0f;
+    }
+    *dst = s;
+}
+
+// W0 (stride 2) dgrad on the zero-padded input domain: dxp (B, H+2, W+2, Cin) gets
+//   dxp[qy][qx] = sum over taps (ty, tx) with qy = 2 Py + ty, qx = 2 Px + tx of G[Py][Px] . W[t]
+// (reflect folding follows in fold_reflect_kernel).  A thread owns 4 input channels of 4
+// same-parity columns qx = px + 2 (4 xg + j), which share the tap set, so one float4 weight
+// load feeds 16 FMAs.  G (B, h, w, Gc) NHWC, WT [9][Cout][Cin]; Cin, Cout, Gc, Goff % 4 == 0.
+__global__ __launch_bounds__(256) void dgrad_s2_kernel(const float *G, int Gc, int Goff, const float *WT, int Cout,
+                                                       int Cin, int B, int h, int w, float *dxp, int Hp, int Wp) {
+    const int cq = Cin >> 2;
+    const int ngx = (((Wp + 1) >> 1) + 3) >> 2;
+    const long total = (long)B * Hp * 2 * ngx * cq;
+    long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int ci = (int)(idx % cq) * 4;
+    idx /= cq;
+    const int xg = (int)(idx % ngx);
+    idx /= ngx;
+    const int px = (int)(idx & 1);
+    idx >>= 1;
+    const int qy = (int)(idx % Hp);
+    const int b = (int)(idx / Hp);
+    const int cnt = (Wp - px + 1) >> 1;
+    if (4 * xg >= cnt) return;
+    float4 acc[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int ty = 0; ty < 3; ++ty) {
+        if ((qy - ty) & 1) continue;
+        const int Py = (qy - ty) >> 1;
+        if (Py < 0 || Py >= h) continue;
+        const float *grow = G + ((size_t)b * h + Py) * w * Gc + Goff;
+        for (int tx = px; tx < 3; tx += 2) {
+            const int pofs = 4 * xg + ((px - tx) >> 1);     // Px of column j = pofs + j
+            bool ok[4];
+            const float *gp[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int Px = pofs + j;
+                ok[j] = Px >= 0 && Px < w && 4 * xg + j < cnt;
+                gp[j] = grow + (size_t)(ok[j] ? Px : 0) * Gc;
+            }
+            const float *wt = WT + (size_t)(ty * 3 + tx) * Cout * Cin + ci;
+            for (int co = 0; co < Cout; co += 4) {
+                float4 wv[4];
+#pragma unroll
+                for (int k = 0; k < 4; ++k) wv[k] = *reinterpret_cast<const float4 *>(wt + (size_t)(co + k) * Cin);
+#pragma unroll
+                for (int j = 0; j < 4; ++j) {
+                    float4 g = *reinterpret_cast<const float4 *>(gp[j] + co);
+                    if (!ok[j]) g = make_float4(0.f, 0.f, 0.f, 0.f);
+                    acc[j].x = fmaf(g.x, wv[0].x, fmaf(g.y, wv[1].x, fmaf(g.z, wv[2].x, fmaf(g.w, wv[3].x, acc[j].x))));
+                    acc[j].y = fmaf(g.x, wv[0].y, fmaf(g.y, wv[1].y, fmaf(g.z, wv[2].y, fmaf(g.w, wv[3].y, acc[j].y))));
+                    acc[j].z = fmaf(g.x, wv[0].z, fmaf(g.y, wv[1].z, fmaf(g.z, wv[2].z, fmaf(g.w, wv[3].z, acc[j].z))));
+                    acc[j].w = fmaf(g.x, wv[0].w, fmaf(g.y, wv[1].w, fmaf(g.z, wv[2].w, fmaf(g.w, wv[3].w, acc[j].w))));
+                }
+            }
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+        const int qx = px + 2 * (4 * xg + j);
+        if (qx < Wp) *reinterpret_cast<float4 *>(dxp + (((size_t)b * Hp + qy) * Wp + qx) * Cin + ci) = acc[j];
+    }
 }
 
 // --------------------------------------------------------------------------------------------
@@ -376,13 +610,21 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
     }
 }
 
-// dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel
-__global__ void lambda_grad_kernel(const float *dlp, int nbl, int C, float *dst, int accumulate) {
-    for (int c = threadIdx.x; c < C; c += blockDim.x) {
-        float s = 0.0f;
-        for (int b = 0; b < nbl; ++b) s += dlp[(size_t)b * C + c];
-        dst[c] = (accumulate ? dst[c] : 0.0f) + s;
+// dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel;
+// one workgroup per channel, tree reduction
+__global__ __launch_bounds__(256) void lambda_grad_kernel(const float *dlp, int nbl, int C, float *dst,
+                                                          int accumulate) {
+    __shared__ float red[256];
+    const int c = blockIdx.x;
+    float s = 0.0f;
+    for (int b = threadIdx.x; b < nbl; b += 256) s += dlp[(size_t)b * C + c];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
     }
+    if (threadIdx.x == 0) dst[c] = (accumulate ? dst[c] : 0.0f) + red[0];
 }
 
 // z = softshrink(v, lambda) (recompute of the ISTA iterate for the D wgrad)
