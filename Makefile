@@ -1,19 +1,27 @@
 # Build of the MI355X (gfx950) hot-path library.  `python -c "import __graft_entry__ as g; g.build()"`
-# drives the same recipe.
+# runs this Makefile.
 HIPCC ?= /opt/rocm/bin/hipcc
 ARCH  ?= gfx950
 HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
 
 LIB  = v2e2v_amd/libcista_hip.so
-SRCS = v2e2v_amd/csrc/cista_abi.hip
-DEPS = $(SRCS) v2e2v_amd/csrc/cista_kernels.hpp v2e2v_amd/csrc/cista_backward.hpp include/cista_lstc.h
+OBJ  = build/cista_abi.o build/cista_voxel.o
 
 all: $(LIB)
 
-$(LIB): $(DEPS)
-	$(HIPCC) $(HIPFLAGS) -shared -o $@ $(SRCS)
+build/cista_abi.o: v2e2v_amd/csrc/cista_abi.hip v2e2v_amd/csrc/cista_kernels.hpp \
+                   v2e2v_amd/csrc/cista_backward.hpp include/cista_lstc.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/cista_voxel.o: v2e2v_amd/csrc/cista_voxel.hip include/cista_voxel.h include/cista_lstc.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+$(LIB): $(OBJ)
+	$(HIPCC) --offload-arch=$(ARCH) -shared -o $@ $(OBJ)
 
 clean:
-	rm -f $(LIB)
+	rm -rf build $(LIB)
 
 .PHONY: all clean

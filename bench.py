@@ -5,8 +5,8 @@ Metric: reconstructed frames/s at 180x240, 5-bin voxels, depth 5, base_channels 
 One STEP = one len_sequence (15) recurrent pass over B sequences per GPU: states carried
 frame to frame, prev_image = previous output (reference test_e2v.py:105-117 semantics),
 starting from prev_states=None / zero image.  Inputs (synthetic voxels, built on the GPU from
-15 000 random events each, reference utils/event_process.py recipe) are resident in HBM before
-the timed region.  value = frames of ALL ranks / max-over-ranks wall time of K steps.
+15 000 random events each by the HIP voxelizer, reference utils/event_process.py) are resident
+in HBM before the timed region; the voxelizer itself is timed separately ("voxelizer").  value = frames of ALL ranks / max-over-ranks wall time of K steps.
 
 Multi-GPU: one process per GPU (torchrun), sequences sharded across ranks with no data-path
 collective (inference replicas: "scaling": "weak"); only the timing max and a barrier use RCCL.
@@ -119,35 +119,61 @@ def train_main(args, torch, vd, rank, world, device):
 
 
 # ------------------------------------------------------------------ synthetic inputs (GPU)
-def synth_voxels(torch, n_frames, n_seq, nb, H, W, n_events, seed, device):
-    """(n_frames, n_seq, nb, H, W) fp32 voxels: per voxel n_events events with sorted
-    t ~ U(0, 0.05), x, y uniform, p in {-1, +1}; temporal-bilinear binning and the nonzero
-    mean/std normalisation with hot-pixel filter (reference utils/event_process.py:15-63,
-    132-154) written with torch ops on the device."""
+def synth_events(torch, n_windows, n_events, H, W, seed, device):
+    """n_windows windows of n_events events each, concatenated: (N, 4) float64 rows (t, x, y, p)
+    with sorted t ~ U(0, 0.05), x, y uniform, p in {0, 1} (SURVEY 8(c)(ii) recipe), generated on
+    the device; offsets (n_windows + 1,) int64."""
     g = torch.Generator(device=device).manual_seed(seed)
-    V = n_frames * n_seq
-    t = torch.sort(torch.rand(V, n_events, generator=g, device=device, dtype=torch.float64) * 0.05, 1)[0]
-    x = torch.randint(0, W, (V, n_events), generator=g, device=device)
-    y = torch.randint(0, H, (V, n_events), generator=g, device=device)
-    p = torch.randint(0, 2, (V, n_events), generator=g, device=device).to(torch.float64) * 2 - 1
-    dT = (t[:, -1:] - t[:, :1]).clamp_min(1e-12)
-    ts = (nb - 1) * (t - t[:, :1]) / dT
-    ti = ts.floor().long()
-    dt = ts - ti
-    base = torch.arange(V, device=device)[:, None] * (nb * H * W) + y * W + x
-    vox = torch.zeros(V * nb * H * W, device=device, dtype=torch.float64)
-    ok = ti < nb
-    vox.index_add_(0, (base + ti * H * W)[ok], (p * (1 - dt))[ok])
-    ok = (ti + 1) < nb
-    vox.index_add_(0, (base + (ti + 1) * H * W)[ok], (p * dt)[ok])
-    vox = vox.view(V, nb * H * W).float()
-    vox[vox.abs() > 25.0 / nb] = 0
-    nz = (vox != 0).float()
-    n = nz.sum(1, keepdim=True).clamp_min(1)
-    mean = vox.sum(1, keepdim=True) / n
-    std = torch.sqrt((vox * vox).sum(1, keepdim=True) / n - mean * mean)
-    vox = nz * (vox - mean) / (std + 1e-8)
-    return vox.view(n_frames, n_seq, nb, H, W).contiguous()
+    t = torch.sort(torch.rand(n_windows, n_events, generator=g, device=device, dtype=torch.float64) * 0.05, 1)[0]
+    x = torch.randint(0, W, (n_windows, n_events), generator=g, device=device).to(torch.float64)
+    y = torch.randint(0, H, (n_windows, n_events), generator=g, device=device).to(torch.float64)
+    p = torch.randint(0, 2, (n_windows, n_events), generator=g, device=device).to(torch.float64)
+    ev = torch.stack([t, x, y, p], -1).view(-1, 4).contiguous()
+    off = torch.arange(0, n_windows * n_events + 1, n_events, dtype=torch.int64, device=device)
+    return ev, off
+
+
+def synth_voxels(torch, n_frames, n_seq, nb, H, W, n_events, seed, device):
+    """(n_frames, n_seq, nb, H, W) fp32 voxels from synthetic events through the HIP voxelizer
+    (events_to_voxel_grid + event_preprocess(filter_hot_pixel=True), reference
+    utils/event_process.py:15-63,132-154)."""
+    from v2e2v_amd import event_process as ep
+    ev, off = synth_events(torch, n_frames * n_seq, n_events, H, W, seed, device)
+    vox = ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, device=device)
+    return vox.view(n_frames, n_seq, nb, H, W)
+
+
+def time_voxelizer(torch, n_windows, n_events, nb, H, W, device, reps=5, cpu_leg=True):
+    """SURVEY 8 row f1, timed separately from the metric: events resident in HBM -> normalised
+    voxels, n_windows windows per call (HIP events on the current stream)."""
+    from v2e2v_amd import event_process as ep
+    ev, off = synth_events(torch, n_windows, n_events, H, W, 99, device)
+    out = torch.empty(n_windows, nb, H, W, device=device)
+    ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    res = {"windows_per_call": n_windows, "events_per_window": n_events, "ms_per_call": round(ms, 3),
+           "windows_per_s": round(n_windows / ms * 1e3, 1),
+           "events_per_s": round(n_windows * n_events / ms * 1e3, 1)}
+    if cpu_leg:
+        # cpu_baseline leg of the voxelizer: the numpy restatement of the reference path (oracle/,
+        # bit-identical to the GPU result), 4 windows on 1 host core; also checks the GPU output
+        from oracle import fixtures as fx
+        evs = ev[: 4 * n_events].cpu().numpy().reshape(4, n_events, 4)
+        t0 = time.perf_counter()
+        ref = [fx.normalize_voxel(fx.voxelize(w, nb, W, H), True) for w in evs]
+        cpu_ms = (time.perf_counter() - t0) / len(evs) * 1e3
+        got = out[:4].cpu().numpy()
+        res["cpu_baseline"] = {"value": round(1e3 / cpu_ms, 1), "unit": "windows/s", "cores": 1, "kind": "port",
+                               "sample": "4 windows of the same workload (numpy restatement)"}
+        res["bit_exact_vs_ref"] = bool(all((g == r).all() for g, r in zip(got, ref)))
+    return res
 
 
 def he_init_(torch, model, seed):
@@ -321,6 +347,9 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
 
+    voxelizer = (time_voxelizer(torch, B * L, args.num_events, 5, H, W, device, cpu_leg=not args.no_cpu_baseline)
+                 if rank == 0 else None)
+
     cpu = None
     psnr_vs_ref = rel_vs_ref = None
     if rank == 0 and not args.no_cpu_baseline:
@@ -357,6 +386,7 @@ def main():
             "layers_ms": {k: round(v["ms"], 4) for k, v in layers.items()},
             "layers_tflops": {k: round(v["tflops"], 1) for k, v in layers.items()},
             "sum_of_kernels_ms_per_frame_batch": round(frame_ms, 3),
+            "voxelizer": voxelizer,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

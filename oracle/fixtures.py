@@ -125,13 +125,19 @@ def voxelize(events: np.ndarray, num_bins: int, W: int, H: int) -> np.ndarray:
     return vox.reshape(num_bins, H, W)
 
 
-def normalize_voxel(vox: np.ndarray, filter_hot_pixel: bool = True) -> np.ndarray:
-    """Restates event_preprocess(mode='std') (reference utils/event_process.py:132-154);
-    computes in float64 like the reference does under numpy 2, returns float32."""
+def normalize_voxel(vox: np.ndarray, filter_hot_pixel: bool = True, mode: str = "std",
+                    per_bin: float = 25.0) -> np.ndarray:
+    """Restates event_preprocess (reference utils/event_process.py:132-154; per_bin=20 gives the
+    hot-pixel threshold of event_preprocess_pytorch :157-162); computes in float64 like the
+    reference does under numpy 2, returns float32."""
     v = vox.astype(np.float32).copy()
     nb = v.shape[0]
     if filter_hot_pixel:
-        v[np.abs(v) > 25.0 / nb] = 0                                # :137-138
+        v[np.abs(v) > per_bin / nb] = 0                             # :137-138
+    if mode == "maxmin":                                            # :139-140
+        return np.asarray((v - v.min()) / (v.max() - v.min() + 1e-8), dtype=np.float32)
+    if mode != "std":
+        return v
     nz = v != 0
     n = nz.sum()
     if n > 0:

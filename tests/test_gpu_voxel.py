@@ -1,0 +1,121 @@
+"""GPU event voxelizer against the reference's numpy path.
+
+Bar: BIT-EXACT.  The golden fixture vox_180x240.npz was produced by the reference's own
+events_to_voxel_grid / event_preprocess (tests/golden/make_golden.py); the oracle restatement
+(oracle/fixtures.py voxelize / normalize_voxel, numpy) is pinned to it by
+tests/test_oracle_golden.py::test_voxelizer_matches_reference and covers the other cases.
+"""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fixtures as fx
+from v2e2v_amd import event_process as ep
+
+pytestmark = pytest.mark.gpu
+
+
+def ref_raw(ev, nb, W, H):
+    return fx.voxelize(ev, nb, W, H)
+
+
+def assert_bits(got, want):
+    got = got.detach().cpu().numpy() if torch.is_tensor(got) else got
+    np.testing.assert_array_equal(got, want)          # -0.0 == 0.0 is fine, NaN never expected
+
+
+def test_golden_180x240_raw_and_std(golden):
+    d = golden("vox_180x240.npz")
+    raw = ep.events_to_voxel_grid(d["events"], 5, 240, 180)
+    assert_bits(raw, d["voxel_raw"])
+    norm = ep.event_preprocess(raw, filter_hot_pixel=True)
+    assert_bits(norm, d["voxel"])
+    fused = ep.events_to_voxel_batch([d["events"]], 5, 240, 180, mode="std", filter_hot_pixel=True)
+    assert_bits(fused[0], d["voxel"])
+
+
+def test_input_not_modified(golden):
+    d = golden("vox_180x240.npz")
+    ev = torch.from_numpy(d["events"].copy()).cuda()
+    before = ev.clone()
+    ep.events_to_voxel_grid(ev, 5, 240, 180)
+    assert torch.equal(ev, before)
+
+
+def _windows(rng, H, W, sizes, hot=False):
+    out = []
+    for n in sizes:
+        ev = fx.synthetic_events(n, H, W, rng)
+        if hot and n > 50:                      # one pixel with many events: order-sensitive sums
+            ev[::3, 1] = 7
+            ev[::3, 2] = 3
+        out.append(ev)
+    return out
+
+
+@pytest.mark.parametrize("H,W,nb", [(64, 64, 5), (32, 48, 3), (180, 240, 5), (31, 17, 7)])
+def test_batch_matches_oracle(H, W, nb):
+    rng = np.random.default_rng(H * W + nb)
+    sizes = [0, 1, 2, 500, 3000, 15000, 7]
+    wins = _windows(rng, H, W, sizes, hot=True)
+    got = ep.events_to_voxel_batch(wins, nb, W, H).cpu().numpy()
+    for b, ev in enumerate(wins):
+        assert_bits(got[b], ref_raw(ev, nb, W, H))
+    for mode in ("std", "maxmin"):
+        for filt in (False, True):
+            got = ep.events_to_voxel_batch(wins, nb, W, H, mode=mode, filter_hot_pixel=filt).cpu().numpy()
+            for b, ev in enumerate(wins):
+                assert_bits(got[b], fx.normalize_voxel(ref_raw(ev, nb, W, H), filt, mode))
+
+
+def test_edge_cases():
+    H, W, nb = 20, 30, 5
+    # all events at one timestamp (deltaT == 0 -> 1.0, reference :40-41), polarity given as -1/1
+    ev0 = np.array([[0.5, 3, 4, 1], [0.5, 3, 4, -1], [0.5, 29, 19, 0], [0.5, 0, 0, 1]], np.float64)
+    # fractional coordinates truncate toward zero (astype(np.uint)); out-of-grid events dropped
+    ev1 = np.array([[0.0, 2.7, 1.2, 1], [0.01, 29.99, 19.5, 0], [0.02, 30.0, 2, 1], [0.03, 1, 20, 1],
+                    [0.04, -0.5, 3, 1], [0.05, 5, 5, 1]], np.float64)
+    ev1_kept = ev1[[0, 1, 4, 5]].copy()
+    ev1_kept[2, 1] = 0.0                         # -0.5 truncates to 0, like the reference's cast
+    got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H).cpu().numpy()
+    assert_bits(got[0], ref_raw(ev0, nb, W, H))
+    assert_bits(got[1], ref_raw(ev1_kept, nb, W, H))
+
+
+def test_preprocess_thresholds_and_batch_shapes():
+    rng = np.random.default_rng(3)
+    H, W, nb = 40, 56, 5
+    wins = _windows(rng, H, W, [4000, 9000, 100])
+    raw = ep.events_to_voxel_batch(wins, nb, W, H)
+    raw[:, :, 5, 5] = 9.0                        # hot pixels above both thresholds
+    raw[:, :, 6, 6] = 4.5                        # between 20/5 and 25/5
+    ref = raw.cpu().numpy()
+    got = ep.event_preprocess(raw, filter_hot_pixel=True).cpu().numpy()
+    for b in range(3):
+        assert_bits(got[b], fx.normalize_voxel(ref[b], True, "std", 25.0))
+    got = ep.event_preprocess_pytorch(raw[1], filter_hot_pixel=True).cpu().numpy()
+    assert_bits(got, fx.normalize_voxel(ref[1], True, "std", 20.0))
+    assert torch.equal(raw.cpu(), torch.from_numpy(ref))      # not modified
+
+
+def test_large_frame_many_events():
+    """720x1280 (the V2E2V resolution, config c5): 563 reduction chunks per window."""
+    rng = np.random.default_rng(11)
+    H, W, nb = 720, 1280, 5
+    ev = fx.synthetic_events(200000, H, W, rng)
+    got = ep.events_to_voxel_batch([ev], nb, W, H, mode="std", filter_hot_pixel=True).cpu().numpy()
+    assert_bits(got[0], fx.normalize_voxel(ref_raw(ev, nb, W, H), True, "std"))
+
+
+def test_device_resident_concatenated_batch():
+    """The (events, offsets) form with everything already in HBM (what bench.py times)."""
+    rng = np.random.default_rng(5)
+    H, W, nb = 180, 240, 5
+    wins = _windows(rng, H, W, [15000] * 16)
+    ev = torch.from_numpy(np.concatenate(wins)).cuda()
+    off = torch.arange(0, 16 * 15000 + 1, 15000, dtype=torch.int64).cuda()
+    got = ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True).cpu().numpy()
+    for b in (0, 7, 15):
+        assert_bits(got[b], fx.normalize_voxel(ref_raw(wins[b], nb, W, H), True, "std"))
+    again = ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True).cpu().numpy()
+    np.testing.assert_array_equal(got, again)       # deterministic

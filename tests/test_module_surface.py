@@ -79,3 +79,19 @@ def test_grad_mode_cpu_raises_no_fallback():
     m = CistaLSTCNet([32, 32], base_channels=32, depth=1, num_bins=5)
     with pytest.raises(RuntimeError, match="ROCm"):
         m(torch.zeros(1, 5, 32, 32), torch.zeros(1, 1, 32, 32), None)
+
+
+def test_voxelizer_surface_cpu():
+    """The voxelizer has no CPU path: CPU input raises; argument errors mirror the reference's
+    asserts (utils/event_process.py:22-25); invalid arguments are rejected by the C ABI."""
+    from v2e2v_amd import event_process as ep
+    from v2e2v_amd import _lib
+    with pytest.raises(RuntimeError, match="ROCm"):
+        ep.event_preprocess(torch.zeros(5, 8, 8))
+    with pytest.raises(AssertionError):
+        ep._as_events(np.zeros((3, 3)), torch.device("cpu"))
+    L = _lib.lib()
+    assert L.cista_voxelize(None, None, 1, 0, 0, 8, 8, 0, 0.0, None, None, 0, None) == 1
+    assert L.cista_voxelize(None, None, 1, 0, 5, 8, 8, 7, 0.0, None, None, 0, None) == 1
+    assert L.cista_voxel_preprocess(None, 1, 5, 8, 8, 3, 0.0, None, 0, None) == 1
+    assert L.cista_voxelize(None, None, 0, 0, 5, 8, 8, 0, 0.0, None, None, 0, None) == 0   # B == 0: no-op

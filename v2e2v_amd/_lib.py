@@ -17,7 +17,8 @@ import torch  # noqa: F401  (must precede the dlopen below, see module docstring
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.environ.get("CISTA_HIP_LIB", os.path.join(_HERE, "libcista_hip.so"))
-HEADER_PATH = os.path.join(os.path.dirname(_HERE), "include", "cista_lstc.h")
+INCLUDE_DIR = os.path.join(os.path.dirname(_HERE), "include")
+HEADER_PATH = os.path.join(INCLUDE_DIR, "cista_lstc.h")
 
 c_int, c_size_t, c_void_p = ctypes.c_int, ctypes.c_size_t, ctypes.c_void_p
 
@@ -99,6 +100,12 @@ def _declare(lib):
                                    P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
+        # include/cista_voxel.h
+        "cista_voxel_workspace_bytes": (c_size_t, [c_int, ctypes.c_longlong, c_int, c_int, c_int]),
+        "cista_voxelize": (c_int, [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_int, c_int, c_int,
+                                   ctypes.c_float, c_void_p, c_void_p, c_size_t, c_void_p]),
+        "cista_voxel_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.c_float,
+                                           c_void_p, c_size_t, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
@@ -126,11 +133,15 @@ def lib():
     return _lib
 
 
-def header_functions(path: str = HEADER_PATH):
-    """Names of every function declared in include/cista_lstc.h."""
-    src = open(path).read()
-    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
-    return sorted(set(re.findall(r"\b(cista_[a-z_]+)\s*\(", src)))
+def header_functions(path: str | None = None):
+    """Names of every function declared in include/*.h (or in one header `path`)."""
+    paths = [path] if path else sorted(
+        os.path.join(INCLUDE_DIR, f) for f in os.listdir(INCLUDE_DIR) if f.endswith(".h"))
+    names = set()
+    for p in paths:
+        src = re.sub(r"/\*.*?\*/", "", open(p).read(), flags=re.S)
+        names |= set(re.findall(r"\b(cista_[a-z_]+)\s*\(", src))
+    return sorted(names)
 
 
 def check(status: int, what: str):
