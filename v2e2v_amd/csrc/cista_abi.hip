@@ -206,7 +206,7 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         if (a.N % 64 == 0) return launch_conv_cfg<2, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N % 32 == 0) return launch_conv_cfg<2, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (EPI == EPI_UP_Q) {      // needs WN == 1
+    } else if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE) {      // needs WN == 1
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
@@ -367,6 +367,7 @@ int run_layer(const Frame &f, int layer, int it = 0) {
             if (up_q_path(C)) {     // + final_conv's channel contraction in the epilogue
                 a.aux0 = blob<float>(f.packed, f.L.wF);
                 a.out1 = f.u;
+                if (f.u) return launch_conv<STAGE_UP, EPI_UP_Q_SAVE, 1>(a, f.st);
                 return launch_conv<STAGE_UP, EPI_UP_Q, 1>(a, f.st);
             }
             return launch_conv<STAGE_UP, EPI_RELU, 1>(a, f.st);

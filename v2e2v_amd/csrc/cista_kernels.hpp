@@ -42,9 +42,10 @@ enum Epi {
     EPI_LSTC_CELL = 4,   // c = sig(f) c_prev + sig(i) z0               (base_layers.py:57-67)
     EPI_LSTC_OUT = 5,    // z = sig(o) tanh(c)                          (base_layers.py:63,69)
     EPI_LSTM = 6,        // c = sig(r) c_prev + sig(i) tanh(g); h = sig(o) tanh(c) (:112-128)
-    EPI_UP_Q = 7         // u = relu(acc + b) -> q_t = sum_c u_c * wf[t][c], t = 0..8: the
+    EPI_UP_Q = 7,        // u = relu(acc + b) -> q_t = sum_c u_c * wf[t][c], t = 0..8: the
                          // final_conv (64->1) contracted over channels in the epilogue, so u
                          // never reaches HBM; the 9 shifted taps are summed by final_q_kernel
+    EPI_UP_Q_SAVE = 8    // EPI_UP_Q that also stores u (out1) for the training backward
 };
 
 struct ConvArgs {
@@ -441,7 +442,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
 
-    if constexpr (EPI == EPI_UP_Q) {
+    if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE) {
         static_assert(WN == 1, "the wave must hold every output channel");
         // values v[t*4 + j] (tap t, accumulator row j) of this lane's channel subset, then a
         // reduce-scatter over the 16 lanes (columns) of each row group: after halving 48 -> 3,
@@ -460,7 +461,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float u = fmaxf(acc[m][n][j] + bz[n], 0.0f);
-                    if (a.out1) {   // training: keep u for the final_conv / ReLU backward
+                    if constexpr (EPI == EPI_UP_Q_SAVE) {   // keep u for the final_conv / ReLU backward
                         const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
                         const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
                         if (p < npix && oy0 + py < a.Hout && ox0 + px < a.Wout)
