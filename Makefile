@@ -5,7 +5,7 @@ ARCH  ?= gfx950
 HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
 
 LIB  = v2e2v_amd/libcista_hip.so
-OBJ  = build/cista_abi.o build/cista_voxel.o
+OBJ  = build/cista_abi.o build/cista_voxel.o build/cista_ssim.o
 
 all: $(LIB)
 
@@ -15,6 +15,10 @@ build/cista_abi.o: v2e2v_amd/csrc/cista_abi.hip v2e2v_amd/csrc/cista_kernels.hpp
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 build/cista_voxel.o: v2e2v_amd/csrc/cista_voxel.hip include/cista_voxel.h include/cista_lstc.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/cista_ssim.o: v2e2v_amd/csrc/cista_ssim.hip include/cista_loss.h include/cista_lstc.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

@@ -62,10 +62,13 @@ def parse():
 def train_main(args, torch, vd, rank, world, device):
     """BPTT training step of train_e2v.py:108-130 on the HIP path: len_sequence frames with
     prev_img = output.clone() (no detach) and states carried, loss on the last frame, one
-    backward through the whole sequence, Adam step.  Loss = L1 (the reference adds LPIPS-VGG,
-    whose weights need a network download, and 1-SSIM: SURVEY 8 row f3, not built).  Multi-GPU:
-    DistributedDataParallel over RCCL (one gradient all-reduce per step)."""
+    backward through the whole sequence, Adam step.  Loss = L1 + (1 - SSIM) as train_e2v.py:
+    117-120 (SSIM on the HIP path, v2e2v_amd/losses.py); the reference also adds LPIPS-VGG, whose
+    weights need a network download.  Multi-GPU: DistributedDataParallel over RCCL
+    (one gradient all-reduce per step)."""
     from v2e2v_amd import CistaLSTCNet
+    from v2e2v_amd.losses import SSIM
+    ssim_fn = SSIM(data_range=1, size_average=True, channel=1, nonnegative_ssim=False)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
     model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
     he_init_(torch, model, seed=7)
@@ -84,7 +87,7 @@ def train_main(args, torch, vd, rank, world, device):
         for s in range(L):
             out, state = net(vox[s], prev, state)
             prev = out.clone()
-        loss = torch.nn.functional.l1_loss(out, target)
+        loss = torch.nn.functional.l1_loss(out, target) + (1 - ssim_fn(out, target))
         opt.zero_grad(set_to_none=True)
         loss.backward()
         opt.step()
@@ -108,7 +111,7 @@ def train_main(args, torch, vd, rank, world, device):
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
-            "data": "synthetic (GPU-generated 15000-event voxels, random targets; L1 loss)",
+            "data": "synthetic (GPU-generated 15000-event voxels, random targets; L1 + 1-SSIM loss)",
             "config": {"workload": f"train_e2v BPTT len {L}, batch {B}/GPU, {H}x{W}",
                        "batch_per_gpu": B, "global_batch": B * world, "len_sequence": L,
                        "parallelism": f"ddp{world}" if world > 1 else "single"},

@@ -9,7 +9,7 @@
  *
  *   cista_pack_params      <- nn.Conv2d parameter storage of CistaLSTCNet.__init__
  *                             (reference e2v/e2v_model.py:6-38); re-run after every
- *                             load_state_dict / optimizer step (weights -> split-bf16 MFMA tiles)
+ *                             load_state_dict / optimizer step (weights -> split-fp16 MFMA fragments)
  *   cista_forward          <- CistaLSTCNet.forward(events, prev_image, prev_states)
  *                             (reference e2v/e2v_model.py:41-90)
  *   cista_stage_input      <- We / Wi / cat / W0                 (e2v_model.py:62-66)
@@ -98,7 +98,7 @@ typedef struct {
 int         cista_abi_version(void);
 const char *cista_status_string(int status);
 
-/* packed (MFMA-tiled, split-bf16) parameter blob */
+/* packed (MFMA-fragment, split-fp16) parameter blob */
 size_t cista_packed_bytes(const cista_config *cfg);
 int    cista_pack_params(const cista_config *cfg, const cista_params *params, void *packed,
                          void *stream);

@@ -111,3 +111,18 @@ def test_stress_recipe_is_deterministic():
     b = fx.stress_params(64, 5, 5)
     assert all(np.array_equal(a[k], b[k]) for k in a)
     assert [k for k, _ in fx.param_shapes()] == list(a.keys())
+
+
+def test_ssim_oracle_properties():
+    """oracle/ssim_oracle.py (parity unpinned: pytorch_msssim is absent): identical images give
+    1, the fp32 and fp64 restatements agree, and the window is the normalised 11-tap Gaussian."""
+    from oracle import ssim_oracle as so
+    g = np.random.default_rng(0)
+    Y = g.uniform(0, 1, (2, 1, 40, 48))
+    X = np.clip(Y + g.normal(0, 0.1, Y.shape), 0, 1)
+    assert abs(so.ssim(Y, Y) - 1.0) < 1e-12
+    s64 = so.ssim(X, Y)
+    s32 = so.ssim(X.astype(np.float32), Y.astype(np.float32))
+    assert 0.0 < s64 < 1.0 and abs(s32 - s64) < 1e-5
+    w = so.gauss_1d()
+    assert w.shape == (11,) and abs(float(w.sum()) - 1.0) < 1e-6 and np.argmax(w) == 5

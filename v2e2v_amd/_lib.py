@@ -106,6 +106,12 @@ def _declare(lib):
                                    ctypes.c_float, c_void_p, c_void_p, c_size_t, c_void_p]),
         "cista_voxel_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.c_float,
                                            c_void_p, c_size_t, c_void_p]),
+        # include/cista_loss.h (config struct passed as a pointer; see losses.CistaSsimConfig)
+        "cista_ssim_workspace_bytes": (c_size_t, [c_int, c_int, c_int, c_int, c_int]),
+        "cista_ssim_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                       c_void_p, c_void_p, c_size_t, c_void_p]),
+        "cista_ssim_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
+                                        c_void_p, c_void_p, c_size_t, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)
