@@ -181,7 +181,11 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
     // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
-    const size_t epi_lds = (size_t)4 * 16 * (NW * 16 + 4) * 4;
+    // the epilogue indexes outputs with 32-bit element offsets (pixel * Cout, x4 for out2)
+    // and the double-buffered staging reads inputs with 32-bit element offsets
+    if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 ? 4 : 1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
+    if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
+    const size_t epi_lds = (size_t)4 * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
     hipLaunchKernelGGL(kern, grid, dim3(256), t.lds > epi_lds ? t.lds : epi_lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }

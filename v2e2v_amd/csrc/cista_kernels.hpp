@@ -233,6 +233,57 @@ __device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4
     }
 }
 
+// Per-thread halo items of the double-buffered loop are the same (hp, g) for every K-chunk, so
+// their source pixel (reflect / zero padding resolved) is computed once per tile; a chunk's
+// load address is then seg + pixel * segC + choff + 8 g in 32-bit arithmetic.
+// spix: pixel index (b, iy, ix) >= 0, -1 = no item, -2 = zero padding (STAGE_ZP2).
+template <int STAGE, int NI>
+__device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd,
+                                             int (&spix)[NI], int (&hps)[NI], int (&gs)[NI]) {
+    const int HP = HH * HWd;
+    const int nitems = ((HP + 7) & ~7) * 4;
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const int it = threadIdx.x + u * 256;
+        const int hp = ((it >> 5) << 3) | (it & 7);
+        gs[u] = (it >> 3) & 3;
+        hps[u] = (it < nitems && hp < HP) ? hp : -1;
+        const int hy = hp / HWd, hx = hp - (hp / HWd) * HWd;
+        int pix = -1;
+        if (hps[u] >= 0) {
+            if constexpr (STAGE == STAGE_ZP2) {
+                const int iy = iy0 + hy, ix = ix0 + hx;
+                pix = (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) ? -2 : (b * a.Hin + iy) * a.Win + ix;
+            } else {
+                const int iy = reflect_clamp(iy0 + hy, a.Hin), ix = reflect_clamp(ix0 + hx, a.Win);
+                pix = (b * a.Hin + iy) * a.Win + ix;
+            }
+        }
+        spix[u] = pix;
+    }
+}
+
+template <int STAGE, int NI>
+__device__ __forceinline__ void stage_issue_px(const ConvArgs &a, const float *seg, int segC, int choff,
+                                               const int (&spix)[NI], const int (&gs)[NI], float4 (&v0)[NI],
+                                               float4 (&v1)[NI]) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        const int pix = spix[u];
+        const unsigned o = (unsigned)(pix < 0 ? 0 : pix) * (unsigned)segC + (unsigned)(choff + gs[u] * 8);
+        v0[u] = *(const float4 *)(seg + o);
+        v1[u] = *(const float4 *)(seg + o + 4);
+        if constexpr (STAGE == STAGE_ZP2) {
+            if (pix == -2) v0[u] = v1[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (a.ascale) {
+                const float sc = a.ascale[0];
+                v0[u].x *= sc; v0[u].y *= sc; v0[u].z *= sc; v0[u].w *= sc;
+                v1[u].x *= sc; v1[u].y *= sc; v1[u].z *= sc; v1[u].w *= sc;
+            }
+        }
+    }
+}
+
 // one tap of one K-chunk: MT_W x NW tiles, 3 split passes each.  Software-pipelined by hand:
 // the A fragments of m-tile m+1 are read while m's MFMAs run, and sched_barrier stops the
 // compiler from hoisting every LDS read of the tap up front (which spills at 256 VGPRs).
@@ -328,10 +379,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     };
     if constexpr (NI > 0) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
+        static_assert(STAGE == STAGE_S1 || STAGE == STAGE_ZP2, "double-buffered staging: stride-1 inputs");
+        int spix[NI], shp[NI], sg[NI];
+        stage_pixels<STAGE, NI>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
         {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
-            stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff);
+            float4 sv0[NI], sv1[NI];
+            stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1);
+            stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg);
         }
         __syncthreads();
         for (int kc = 0; kc < nchunks; ++kc) {
@@ -350,7 +406,6 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                 bl[n] = wp[n * 128 + 64];
             }
             float4 sv0[NI], sv1[NI];
-            int shp[NI], sg[NI];
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 u32x4 nh[NW], nl[NW];
@@ -364,8 +419,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                 }
                 // the next chunk's halo loads go out after B(0), B(1): the waits for those two
                 // do not include them (vmcnt is in order); they land under taps 0..1
-                if (tap == 0 && more)
-                    stage_issue<STAGE, NI>(a, b, iy0, ix0, HH, HWd, nseg, nsegC, nchoff, sv0, sv1, shp, sg);
+                if (tap == 0 && more) stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1);
                 mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
                 if (tap < 8) {
 #pragma unroll
@@ -506,8 +560,31 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     __syncthreads();                                       // staging LDS is free from here on
     constexpr int LDT = NW * 16 + 4;                       // padded row: conflict-free writes
     constexpr int CG = (NW / G) * 4;                       // 4-channel groups per pixel
+    static_assert(64 % CG == 0, "a lane's channel group must be the same for every item");
+    constexpr int NPXB = MT_W * WM * 16;                   // pixels of the workgroup tile
     float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
+    // per-pixel element offset (pixel * Cout) of the output tensors, -1 outside the image:
+    // the items below then need no division, no 64-bit math and no bounds arithmetic
+    int *ptab = reinterpret_cast<int *>(smem) + 4 * 16 * LDT;
+    for (int p = threadIdx.x; p < NPXB; p += 256) {
+        int v = -1;
+        if (p < npix) {
+            const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
+            const int oy = oy0 + py, ox = ox0 + px;
+            if (oy < a.Hout && ox < a.Wout) v = ((b * a.Hout + oy) * a.Wout + ox) * a.Cout;
+        }
+        ptab[p] = v;
+    }
+    __syncthreads();
     const int grp = lane >> 4;
+    // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
+    const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
+    const int ch = ((nt0 / G) + q) * 16 + c4;              // channel within a gate
+    float4 bias4[G];
+#pragma unroll
+    for (int g = 0; g < G; ++g) bias4[g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + c4);
+    float4 lam4 = make_float4(0.f, 0.f, 0.f, 0.f);
+    if constexpr (EPI == EPI_ISTA_P) lam4 = *(const float4 *)(a.lambda + ch);
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
 #pragma unroll
@@ -519,26 +596,18 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 #pragma unroll
         for (int it0 = 0; it0 < 16 * CG; it0 += 64) {
-            const int it = it0 + lane;
-            if (it < 16 * CG) {
-                const int row = it / CG, cg = it - row * CG;
-                const int q = cg >> 2, c4 = (cg & 3) * 4;
-                const int p = (wm * MT_W + m) * 16 + row;
-                const int py = p / a.TW;
-                const int px = p - py * a.TW;
-                const int oy = oy0 + py, ox = ox0 + px;
-                if (p < npix && oy < a.Hout && ox < a.Wout) {
-                    const size_t pix = ((size_t)b * a.Hout + oy) * a.Wout + ox;
+            {
+                const int row = (it0 + lane) / CG;
+                const int off = ptab[(wm * MT_W + m) * 16 + row];
+                if (off >= 0) {
                     float4 v[G];
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
-                        const int nl = q * G + g;                      // n-tile within the wave
-                        const float *src = T + row * LDT + nl * 16 + c4;
-                        const float4 bb = *(const float4 *)(a.bias + (nt0 + nl) * 16 + c4);
-                        v[g] = make_float4(src[0] + bb.x, src[1] + bb.y, src[2] + bb.z, src[3] + bb.w);
+                        const float *src = T + row * LDT + (q * G + g) * 16 + c4;
+                        v[g] = make_float4(src[0] + bias4[g].x, src[1] + bias4[g].y, src[2] + bias4[g].z,
+                                           src[3] + bias4[g].w);
                     }
-                    const int ch = ((nt0 / G) + q) * 16 + c4;          // channel within a gate
-                    const size_t o = pix * a.Cout + ch;
+                    const unsigned o = (unsigned)off + (unsigned)ch;
                     float r[4], r1[4];
                     const float *vv = reinterpret_cast<const float *>(v);
                     if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
@@ -551,9 +620,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
                     } else if constexpr (EPI == EPI_ISTA_P) {
                         const float4 z = *(const float4 *)(a.aux0 + o);
-                        const float4 lm = *(const float4 *)(a.lambda + ch);
                         const float *zz = reinterpret_cast<const float *>(&z);
-                        const float *ll = reinterpret_cast<const float *>(&lm);
+                        const float *ll = reinterpret_cast<const float *>(&lam4);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
                             const float x = vv[e] + zz[e];
@@ -604,7 +672,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         }
                         *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                         if (a.out2) {
-                            float *gsv = a.out2 + pix * 4 * a.Cout + ch;
+                            float *gsv = a.out2 + 4u * (unsigned)off + (unsigned)ch;
                             *(float4 *)(gsv) = make_float4(gi[0], gi[1], gi[2], gi[3]);
                             *(float4 *)(gsv + a.Cout) = make_float4(gr[0], gr[1], gr[2], gr[3]);
                             *(float4 *)(gsv + 2 * a.Cout) = make_float4(go[0], go[1], go[2], go[3]);
