@@ -585,8 +585,30 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     for (int g = 0; g < G; ++g) bias4[g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + c4);
     float4 lam4 = make_float4(0.f, 0.f, 0.f, 0.f);
     if constexpr (EPI == EPI_ISTA_P) lam4 = *(const float4 *)(a.lambda + ch);
+    // aux inputs of m-tile m+1 are loaded before m-tile m's stores go out: vmcnt counts loads
+    // and stores in order, so a load issued after a store would also wait for that store (and
+    // ISTA_P updates z in place, so the compiler may not reorder them itself)
+    constexpr int NIT = 16 * CG / 64;                      // items per lane per m-tile
+    constexpr bool USE_A0 = EPI == EPI_ISTA_D || EPI == EPI_ISTA_P || EPI == EPI_LSTC_OUT ||
+                            EPI == EPI_LSTC_CELL || EPI == EPI_LSTM;
+    constexpr bool USE_A1 = EPI == EPI_LSTC_CELL;
+    auto load_aux = [&](int m, float4 (&A0)[NIT], float4 (&A1)[NIT]) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
+            const unsigned o = (unsigned)(off < 0 ? 0 : off) + (unsigned)ch;
+            A0[it] = A1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if constexpr (USE_A0)
+                if (a.aux0) A0[it] = *(const float4 *)(a.aux0 + o);
+            if constexpr (USE_A1) A1[it] = *(const float4 *)(a.aux1 + o);
+        }
+    };
+    float4 curA0[NIT], curA1[NIT];
+    load_aux(0, curA0, curA1);
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
+        float4 nxtA0[NIT], nxtA1[NIT];
+        if (m + 1 < MT_W) load_aux(m + 1, nxtA0, nxtA1);
 #pragma unroll
         for (int n = 0; n < NW; ++n)
 #pragma unroll
@@ -614,12 +636,12 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? fmaxf(vv[e], 0.0f) : vv[e];
                     } else if constexpr (EPI == EPI_ISTA_D) {
-                        const float4 x1 = *(const float4 *)(a.aux0 + o);
+                        const float4 x1 = curA0[it0 / 64];
                         const float *xx = reinterpret_cast<const float *>(&x1);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
                     } else if constexpr (EPI == EPI_ISTA_P) {
-                        const float4 z = *(const float4 *)(a.aux0 + o);
+                        const float4 z = curA0[it0 / 64];
                         const float *zz = reinterpret_cast<const float *>(&z);
                         const float *ll = reinterpret_cast<const float *>(&lam4);
 #pragma unroll
@@ -630,7 +652,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         }
                         if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_OUT) {
-                        const float4 c = *(const float4 *)(a.aux0 + o);
+                        const float4 c = curA0[it0 / 64];
                         const float *cc = reinterpret_cast<const float *>(&c);
 #pragma unroll
                         for (int e = 0; e < 4; ++e) {
@@ -640,8 +662,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_CELL) {
                         // packed n-tile order per channel block: (in, forget)
-                        const float4 z0 = *(const float4 *)(a.aux1 + o);
-                        const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float4 z0 = curA1[it0 / 64];
+                        const float4 cp = curA0[it0 / 64];
                         const float *zz = reinterpret_cast<const float *>(&z0);
                         const float *pp = reinterpret_cast<const float *>(&cp);
                         float si[4], sf[4];
@@ -657,7 +679,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         }
                     } else if constexpr (EPI == EPI_LSTM) {
                         // packed n-tile order per channel block: (in, remember, out, cell)
-                        const float4 cp = a.aux0 ? *(const float4 *)(a.aux0 + o) : make_float4(0.f, 0.f, 0.f, 0.f);
+                        const float4 cp = curA0[it0 / 64];
                         const float *pp = reinterpret_cast<const float *>(&cp);
                         float gi[4], gr[4], go[4], gg[4];
 #pragma unroll
@@ -681,6 +703,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                     }
                     *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
                 }
+            }
+        }
+        if (m + 1 < MT_W) {
+#pragma unroll
+            for (int it = 0; it < NIT; ++it) {
+                curA0[it] = nxtA0[it];
+                curA1[it] = nxtA1[it];
             }
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
