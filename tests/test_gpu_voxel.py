@@ -119,3 +119,23 @@ def test_device_resident_concatenated_batch():
         assert_bits(got[b], fx.normalize_voxel(ref_raw(wins[b], nb, W, H), True, "std"))
     again = ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True).cpu().numpy()
     np.testing.assert_array_equal(got, again)       # deterministic
+
+
+def test_gpu_voxel_loader_matches_reference_path(tmp_path):
+    """f4: the GPU loader yields what train_data_loaders.py:187-193 computes per window
+    (voxelize + event_preprocess(filter_hot_pixel=False)), bit-exact, in the (step, batch) layout
+    of train_e2v.py:104-112."""
+    from tests.test_data_readers import make_dataset
+    from v2e2v_amd import data
+    ds = make_dataset(tmp_path, n_lines=24)
+    loader = data.GpuVoxelLoader(ds, "cuda", batch_size=2, shuffle=False, num_workers=0)
+    seq_events, img, gt = next(iter(loader))
+    assert len(seq_events) == 5 and seq_events[0].shape == (2, 5, 24, 32) and img.shape == (2, 1, 24, 32)
+    for b in range(2):
+        events, sizes, _, _ = ds[b]
+        off = 0
+        for s in range(5):
+            win = events[off:off + int(sizes[s])].numpy()
+            off += int(sizes[s])
+            ref = fx.normalize_voxel(fx.voxelize(win, 5, 32, 24), filter_hot_pixel=False)
+            assert_bits(seq_events[s][b], ref)

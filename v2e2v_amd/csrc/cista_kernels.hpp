@@ -33,6 +33,25 @@ typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // STAGE_ZP2: dgrad correlation -- zero padding of 2, output on the padded input domain (H+2)
+// Timing-only experiment switches (scripts/ab_layers.sh builds; results are WRONG when on):
+//   CISTA_EXP_NOB      B fragments of tap 0 reused for every tap (no per-tap L2 loads)
+//   CISTA_EXP_NOA      one A fragment per tap reused for every m-tile (no per-m LDS reads)
+//   CISTA_EXP_NOSTAGE  halo staged only for the first K-chunk
+//   CISTA_EXP_NOEPI    epilogue stores skipped
+#ifndef CISTA_EXP_NOB
+#define CISTA_EXP_NOB 0
+#endif
+#ifndef CISTA_EXP_NOA
+#define CISTA_EXP_NOA 0
+#endif
+#ifndef CISTA_EXP_NOSTAGE
+#define CISTA_EXP_NOSTAGE 0
+#endif
+#ifndef CISTA_EXP_NOEPI
+#define CISTA_EXP_NOEPI 0
+#endif
+
+
 enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2, STAGE_ZP2 = 3 };
 enum Epi {
     EPI_BIAS = 0,        // out = acc + b
@@ -296,9 +315,12 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
     al[0] = smem[4 * HPpad + abase[0] + toff];
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        if (m + 1 < MT_W) {
+        if (m + 1 < MT_W && !CISTA_EXP_NOA) {
             ah[(m + 1) & 1] = smem[abase[m + 1] + toff];
             al[(m + 1) & 1] = smem[4 * HPpad + abase[m + 1] + toff];
+        } else if (m + 1 < MT_W) {
+            ah[(m + 1) & 1] = ah[m & 1];
+            al[(m + 1) & 1] = al[m & 1];
         }
         const f16x8 xh = __builtin_bit_cast(f16x8, ah[m & 1]);
         const f16x8 xl = __builtin_bit_cast(f16x8, al[m & 1]);
@@ -409,17 +431,24 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 u32x4 nh[NW], nl[NW];
-                if (tap < 8) {
+                if (tap < 8 && !CISTA_EXP_NOB) {
                     const u32x4 *wq = wp + (size_t)(tap + 1) * tapstride;
 #pragma unroll
                     for (int n = 0; n < NW; ++n) {
                         nh[n] = wq[n * 128];
                         nl[n] = wq[n * 128 + 64];
                     }
+                } else if (tap < 8) {
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        nh[n] = bh[n];
+                        nl[n] = bl[n];
+                    }
                 }
                 // the next chunk's halo loads go out after B(0), B(1): the waits for those two
                 // do not include them (vmcnt is in order); they land under taps 0..1
-                if (tap == 0 && more) stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1);
+                if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
+                    stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1);
                 mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
                 if (tap < 8) {
 #pragma unroll
@@ -429,7 +458,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                     }
                 }
             }
-            if (more) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg);
+            if (more && !CISTA_EXP_NOSTAGE) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg);
             __syncthreads();
         }
     } else
@@ -605,6 +634,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     };
     float4 curA0[NIT], curA1[NIT];
     load_aux(0, curA0, curA1);
+    // results are kept in registers (acc[m]'s registers die as res[m] is born) and stored in
+    // one burst after the last aux load: no load then waits behind an outstanding store
+    float4 res[MT_W][NIT];
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
         float4 nxtA0[NIT], nxtA1[NIT];
@@ -701,7 +733,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             *(float4 *)(gsv + 3 * a.Cout) = make_float4(gg[0], gg[1], gg[2], gg[3]);
                         }
                     }
-                    *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
+                    res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
                 }
             }
         }
@@ -716,6 +748,14 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     }
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
+            if (off >= 0 && (CISTA_EXP_NOEPI == 0 || res[m][it].x == 12345.f))
+                *(float4 *)(a.out0 + (unsigned)off + (unsigned)ch) = res[m][it];
+        }
 }
 
 // ------------------------------------------------------------------------------------------
