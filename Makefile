@@ -5,7 +5,7 @@ ARCH  ?= gfx950
 HIPFLAGS = -O3 -std=c++17 --offload-arch=$(ARCH) -fPIC -Wall -Wno-unused-result
 
 LIB  = v2e2v_amd/libcista_hip.so
-OBJ  = build/cista_abi.o build/cista_voxel.o build/cista_ssim.o
+OBJ  = build/cista_abi.o build/cista_voxel.o build/cista_ssim.o build/cista_v2e.o
 
 all: $(LIB)
 
@@ -19,6 +19,10 @@ build/cista_voxel.o: v2e2v_amd/csrc/cista_voxel.hip include/cista_voxel.h includ
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 
 build/cista_ssim.o: v2e2v_amd/csrc/cista_ssim.hip include/cista_loss.h include/cista_lstc.h
+	@mkdir -p build
+	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
+
+build/cista_v2e.o: v2e2v_amd/csrc/cista_v2e.hip include/cista_v2e.h include/cista_voxel.h include/cista_lstc.h
 	@mkdir -p build
 	$(HIPCC) $(HIPFLAGS) -c -o $@ $<
 

@@ -126,3 +126,20 @@ def test_ssim_oracle_properties():
     assert 0.0 < s64 < 1.0 and abs(s32 - s64) < 1e-5
     w = so.gauss_1d()
     assert w.shape == (11,) and abs(float(w.sum()) - 1.0) < 1e-6 and np.argmax(w) == 5
+
+
+def test_v2e_oracle_properties():
+    """oracle/v2e_oracle.py (parity unpinned): lin_log's two branches, no events from a static
+    scene in the deterministic configuration, and ON/OFF events with the right sign."""
+    from oracle import v2e_oracle as vo
+    x = np.array([0.0, 10.0, 20.0, 100.0], np.float32)
+    np.testing.assert_allclose(vo.lin_log(x), [0.0, 10 * np.log(20) / 20, np.log(20), np.log(100)], rtol=1e-7)
+    det = dict(sigma_thres=0.0, leak_rate_hz=0.0, shot_noise_rate_hz=0.0)
+    static = np.full((1, 5, 8, 8), 100.0, np.float32)
+    vox, n = vo.V2EOracle(**det).forward(static, np.linspace(0, 0.04, 5)[None])
+    assert n == 0 and not vox.any()
+    ramp = np.stack([np.full((8, 8), 30.0 * (1.3 ** k), np.float32) for k in range(5)])[None]
+    vox, n = vo.V2EOracle(**det).forward(ramp, np.linspace(0, 0.04, 5)[None])
+    assert n > 0 and vox.min() >= 0 and vox.max() > 0            # brightening: ON events only
+    vox, _ = vo.V2EOracle(**det).forward(ramp[:, ::-1].copy(), np.linspace(0, 0.04, 5)[None])
+    assert vox.max() <= 0 and vox.min() < 0

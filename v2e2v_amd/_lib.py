@@ -112,6 +112,11 @@ def _declare(lib):
                                        c_void_p, c_void_p, c_size_t, c_void_p]),
         "cista_ssim_backward": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p,
                                         c_void_p, c_void_p, c_size_t, c_void_p]),
+        # include/cista_v2e.h (config / host-state structs: v2e2v_amd/v2e.py)
+        "cista_v2e_state_bytes": (c_size_t, [c_int, c_int, c_int]),
+        "cista_v2e_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+        "cista_v2e_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
+                                      c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

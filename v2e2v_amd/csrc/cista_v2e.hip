@@ -1,0 +1,419 @@
+// GPU video-to-events emulator, voxel-grid mode; contract in
+// include/cista_v2e.h.  Reference: v2e/v2e_model.py:290-536, v2e/emulator_utils.py:13-207.
+//
+// Per forward call:
+//   v2e_init_kernel   (first call)  base = lp = lin_log(frame 0), thresholds, noise rates, the
+//                                   refractory memory                            (_init :158-253)
+//   v2e_tmem_kernel   (later calls) refractory memory shifted by one voxel span    (:329-331)
+//   per frame n = 1 .. F-1:
+//     v2e_diff_kernel  low-pass (:266-289), leak (:361-368), diff / polarity / threshold / event
+//                      count (:393-413), image max of the counts per batch element
+//     v2e_iters_kernel num_iters, ts_step, max_num_iters, refractory switch    (:414-427,447)
+//     v2e_emit_kernel  the per-iteration emission (:436-492) with shot noise (:437-440), the
+//                      refractory filter and the voxel accumulation in this pixel's own voxels,
+//                      then base += pol * n_events * C                           (:520)
+//   event_preprocess_pytorch('std') over the whole tensor                        (:526)
+//
+// Floating-point contraction is off: every expression rounds like the reference's float32 ops.
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+
+#include "../../include/cista_lstc.h"
+#include "../../include/cista_v2e.h"
+#include "../../include/cista_voxel.h"
+
+namespace cista_v2e {
+
+// ------------------------------------------------------------------ Philox4x32-10 stream
+struct U4 {
+    unsigned x, y, z, w;
+};
+
+__device__ __forceinline__ U4 philox(U4 c, unsigned k0, unsigned k1) {
+#pragma unroll
+    for (int r = 0; r < 10; ++r) {
+        const unsigned hi0 = __umulhi(0xD2511F53u, c.x), lo0 = 0xD2511F53u * c.x;
+        const unsigned hi1 = __umulhi(0xCD9E8D57u, c.z), lo1 = 0xCD9E8D57u * c.z;
+        c = U4{hi1 ^ c.y ^ k0, lo1, hi0 ^ c.w ^ k1, lo0};
+        k0 += 0x9E3779B9u;
+        k1 += 0xBB67AE85u;
+    }
+    return c;
+}
+
+__device__ __forceinline__ float u01(unsigned u) { return ((float)(u >> 8) + 0.5f) * (1.0f / 16777216.0f); }
+
+// draw `d` of element `e`: a uniform and a standard normal
+__device__ __forceinline__ U4 draw(unsigned long long seed, unsigned long long d, unsigned long long e) {
+    return philox(U4{(unsigned)e, (unsigned)(e >> 32), (unsigned)d, (unsigned)(d >> 32)}, (unsigned)seed,
+                  (unsigned)(seed >> 32));
+}
+__device__ __forceinline__ float randn(unsigned long long seed, unsigned long long d, unsigned long long e) {
+    const U4 r = draw(seed, d, e);
+    return sqrtf(-2.0f * logf(u01(r.x))) * cosf(6.28318530717958647692f * u01(r.y));
+}
+__device__ __forceinline__ float rand01(unsigned long long seed, unsigned long long d, unsigned long long e) {
+    return u01(draw(seed, d, e).x);
+}
+
+// ------------------------------------------------------------------ per-call constants
+struct Call {
+    int B, F, H, W, nb;
+    float tf[CISTA_V2E_MAX_FRAMES];            // t_float_frames (:313-317)
+    float time_frames[CISTA_V2E_MAX_FRAMES];   // voxel-time of each frame (:319-320)
+    float Tr[CISTA_V2E_MAX_BATCH];             // refractory period in voxel time (:322)
+    float dt_lp0[CISTA_V2E_MAX_FRAMES];        // delta_time / tau0 per frame (low-pass, ql)
+    float dt_lp1[CISTA_V2E_MAX_FRAMES];        // delta_time / tau1 per frame (qs)
+    float duration;                            // (nb - 1) / (F - 1) as float32
+    double linlog_f;                           // (1 / 20) * log(20)
+    unsigned long long seed, draw0;
+    cista_v2e_config cfg;
+};
+
+struct State {   // device planes, B*H*W each
+    float *base, *lp, *pos, *neg, *pos_pre, *neg_pre, *noise_rate, *tmem;
+};
+
+struct Scratch {
+    int *counts;          // B*H*W event counts of the current frame
+    float *pol;           // B*H*W polarity (+1 / -1 / 0)
+    int *iters_raw;       // [B] image max of counts
+    int *num_iters;       // [B] max(iters_raw, 1)
+    float *ts_step;       // [B]
+    int *meta;            // [0] max_num_iters, [1] refractory switch
+    unsigned long long *nev;
+};
+
+__device__ __forceinline__ float lin_log(float v, double f) {
+    // emulator_utils.py:13-38 (float64, rounded to 8 decimals, half to even like torch.round)
+    const double x = (double)v;
+    double y = x <= 20.0 ? x * f : log(x);
+    y = rint(y * 1e8) / 1e8;
+    return (float)y;
+}
+__device__ __forceinline__ float rescale(float v) { return (v + 20.0f) / 275.0f; }   // :41-46
+
+__global__ void v2e_init_kernel(Call c, State s, const float *frames) {
+    const long long HW = (long long)c.H * c.W;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)c.B * HW) return;
+    const int b = (int)(i / HW);
+    const long long p = i - b * HW;
+    const int y = (int)(p / c.W), x = (int)(p - (long long)y * c.W);
+    const float l0 = lin_log(frames[((long long)b * c.F) * HW + p], c.linlog_f);
+    s.base[i] = l0;
+    s.lp[i] = l0;
+    const cista_v2e_config &g = c.cfg;
+    float pt = g.pos_thres, nt = g.neg_thres;
+    if (g.sigma_thres > 0.0f) {
+        const bool half = (y % 2 == 0) && (x % 2 == 0);   // [:, :, 0::2, 0::2] (:213,226)
+        const float pm = (half ? g.ps : g.pl) * g.pos_thres, nm = (half ? g.ps : g.pl) * g.neg_thres;
+        pt = fmaxf(pm + g.sigma_thres * randn(c.seed, c.draw0 + (half ? 1 : 0), i), 0.01f);
+        nt = fmaxf(nm + g.sigma_thres * randn(c.seed, c.draw0 + (half ? 3 : 2), i), 0.01f);
+    }
+    s.pos[i] = pt;
+    s.neg[i] = nt;
+    s.pos_pre[i] = pt * (1.0f / g.pos_thres);                 // einsum(1 / nominal, thres) (:232)
+    s.neg_pre[i] = nt * (1.0f / g.neg_thres);
+    if (g.leak_rate_hz > 0.0f)                                 // log-normal rates (:244-248)
+        s.noise_rate[i] = expf((float)(2.302585092994046 * g.noise_rate_cov_decades) * randn(c.seed, c.draw0 + 4, i));
+    s.tmem[i] = 0.0f - c.Tr[b];                                // (:252)
+}
+
+__global__ void v2e_tmem_kernel(Call c, State s) {
+    const long long HW = (long long)c.H * c.W;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= (long long)c.B * HW) return;
+    float t = s.tmem[i];
+    if (t > 0.0f) t -= (float)(c.nb - 1);                      // :330
+    if (t < 0.0f) t = -c.Tr[i / HW];                           // :331
+    s.tmem[i] = t;
+}
+
+__global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch w, const float *frames, int n,
+                                                       float dt_frame) {
+    const long long HW = (long long)c.H * c.W;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const cista_v2e_config &g = c.cfg;
+    int cnt = 0;
+    int b = 0;
+    if (i < (long long)c.B * HW) {
+        b = (int)(i / HW);
+        const long long p = i - b * HW;
+        const int y = (int)(p / c.W), x = (int)(p - (long long)y * c.W);
+        const float fr = frames[((long long)b * c.F + n) * HW + p];
+        float nw = lin_log(fr, c.linlog_f);
+        if (g.cutoff_hz > 0.0f) {                              // low_pass_filter (:49-101)
+            const float inten = rescale(fr);
+            const bool half = (y % 2 == 0) && (x % 2 == 0);
+            float eps = g.ql > 0.0f ? inten * c.dt_lp0[n] : 1.0f;
+            if (half) eps = g.qs > 0.0f ? inten * c.dt_lp1[n] : 1.0f;
+            eps = fminf(eps, 1.0f);
+            nw = (1.0f - eps) * s.lp[i] + eps * nw;
+            s.lp[i] = nw;
+        }
+        float base = s.base[i];
+        if (g.leak_rate_hz > 0.0f) {                           // subtract_leak_current (:104-124)
+            const float r = randn(c.seed, c.draw0 + 8 + 2 * (unsigned long long)n, i);
+            const float rate = g.leak_rate_hz * s.noise_rate[i] * (1.0f - g.leak_jitter_fraction * r);
+            base = base - dt_frame * rate * s.pos[i];
+            s.base[i] = base;
+        }
+        float diff = nw - base;                                // :386
+        if (!(fabsf(diff) > 1e-6f)) diff = 0.0f;               // :405-406
+        const float pol = diff > 0.0f ? 1.0f : (diff < 0.0f ? -1.0f : 0.0f);
+        const float C = (pol > 0.0f ? s.pos[i] : 0.0f) + (pol < 0.0f ? s.neg[i] : 0.0f);   // :412
+        cnt = (int)floorf(fabsf(diff) / (C + 1e-9f));          // :413
+        w.counts[i] = cnt;
+        w.pol[i] = pol;
+    }
+    // image max of the counts per batch element: wave max, then one atomic per wave (exact)
+    int m = cnt;
+    for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
+    const int b0 = __shfl(b, 0);
+    const bool uniform = __all(b == b0);
+    if (uniform) {
+        if ((threadIdx.x & 63) == 0 && i - (threadIdx.x & 63) < (long long)c.B * HW) atomicMax(w.iters_raw + b0, m);
+    } else if (i < (long long)c.B * HW) {
+        atomicMax(w.iters_raw + b, cnt);
+    }
+}
+
+__global__ void v2e_iters_kernel(Call c, Scratch w) {
+    if (threadIdx.x != 0) return;
+    int mx = 0;
+    for (int b = 0; b < c.B; ++b) {
+        const int r = w.iters_raw[b];
+        mx = max(mx, r);                                       // max_num_iters (:417)
+        const int ni = r == 0 ? 1 : r;                         // :426
+        w.num_iters[b] = ni;
+        w.ts_step[b] = c.duration / (float)ni;                 // :427
+    }
+    int refr = 0;                                              // (Tr > ts_step).any(), (B,1) vs (B,)
+    for (int b1 = 0; b1 < c.B; ++b1)
+        for (int b2 = 0; b2 < c.B; ++b2) refr |= c.Tr[b1] > w.ts_step[b2];
+    w.meta[0] = mx;
+    w.meta[1] = refr;
+}
+
+__global__ __launch_bounds__(256) void v2e_emit_kernel(Call c, State s, Scratch w, const float *frames, float *vox,
+                                                       int n, float dt_frame) {
+    const long long HW = (long long)c.H * c.W;
+    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const cista_v2e_config &g = c.cfg;
+    unsigned long long nev = 0;
+    if (i < (long long)c.B * HW) {
+        const int b = (int)(i / HW);
+        const long long p = i - b * HW;
+        const int cnt = w.counts[i];
+        const float pol = w.pol[i];
+        const int max_iters = w.meta[0];
+        const bool refr = w.meta[1] != 0;
+        const int ni = w.num_iters[b];
+        const float step = w.ts_step[b];
+        const float Tr = c.Tr[b];
+        const float C = (pol > 0.0f ? s.pos[i] : 0.0f) + (pol < 0.0f ? s.neg[i] : 0.0f);
+        // shot noise thresholds (generate_shot_noise, emulator_utils.py:159-207)
+        float on_thr = 1.0f, off_thr = 0.0f;
+        const bool shot = g.shot_noise_rate_hz > 0.0f && pol != 0.0f;
+        if (shot) {
+            const float inten = rescale(frames[((long long)b * c.F + n) * HW + p]);
+            const float factor = (g.shot_noise_rate_hz / 2.0f * dt_frame / (float)ni) * ((0.25f - 1.0f) * inten + 1.0f);
+            on_thr = 1.0f - factor * s.pos_pre[i];
+            off_thr = factor * s.neg_pre[i];
+        }
+        float tmem = s.tmem[i];
+        int final_cnt = 0;
+        float *vp = vox + (size_t)b * c.nb * HW + p;
+        const float t0 = c.time_frames[n - 1];
+        for (int it = 0; it < max_iters; ++it) {
+            bool m = cnt >= it + 1;                            // :459
+            if (shot && it < ni) {                             // num_iter_mask (:196-198)
+                const float r = rand01(c.seed, c.draw0 + 9 + 2 * (unsigned long long)n,
+                                       ((unsigned long long)it * c.B + b) * HW + p);
+                m = m || (pol > 0.0f ? r > on_thr : r < off_thr);
+            }
+            const float ts = it < ni ? t0 + step * (float)(it + 1) : 0.0f;   // :428-432
+            if (refr) {                                        // :469-473
+                const float since = ts * (m ? 1.0f : 0.0f) - tmem;
+                m = since > Tr;
+                if (m) tmem = ts;
+            }
+            if (!m) continue;
+            final_cnt += 1;                                    // :476
+            const float ti = floorf(ts);                       // :479-484
+            const float dts = ts - ti;
+            if (ti >= 0.0f) {
+                const int k = (int)ts;
+                nev += 1;
+                if (k < c.nb) vp[(size_t)k * HW] += pol * (1.0f - dts);   // k >= nb: dropped
+                if (ti + 1.0f < (float)c.nb) vp[(size_t)(k + 1) * HW] += pol * dts;
+            }
+        }
+        if (refr) s.tmem[i] = tmem;
+        s.base[i] = s.base[i] + pol * (float)final_cnt * C;   // :520
+    }
+    // events generated: block reduction then one atomic
+    __shared__ unsigned long long red[256];
+    red[threadIdx.x] = nev;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0 && red[0]) atomicAdd(w.nev, red[0]);
+}
+
+inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
+
+State carve_state(void *base, int B, int H, int W) {
+    State s;
+    size_t off = 0;
+    const size_t n = (size_t)B * H * W;
+    char *p = static_cast<char *>(base);
+    auto take = [&]() {
+        float *r = p ? reinterpret_cast<float *>(p + off) : nullptr;
+        off = align_up(off + n * 4);
+        return r;
+    };
+    s.base = take(); s.lp = take(); s.pos = take(); s.neg = take();
+    s.pos_pre = take(); s.neg_pre = take(); s.noise_rate = take(); s.tmem = take();
+    (void)off;
+    return s;
+}
+
+size_t state_bytes(int B, int H, int W) { return 8 * align_up((size_t)B * H * W * 4); }
+
+struct WsLayout {
+    Scratch sc;
+    void *vox_ws;       // voxel preprocess workspace
+    size_t vox_ws_bytes, bytes;
+};
+
+WsLayout carve_ws(void *base, int B, int H, int W, int nb) {
+    WsLayout L;
+    size_t off = 0;
+    const size_t n = (size_t)B * H * W;
+    char *p = static_cast<char *>(base);
+    auto take = [&](size_t bytes) {
+        void *r = p ? p + off : nullptr;
+        off = align_up(off + bytes);
+        return r;
+    };
+    L.sc.counts = static_cast<int *>(take(n * 4));
+    L.sc.pol = static_cast<float *>(take(n * 4));
+    L.sc.iters_raw = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * 4));
+    L.sc.num_iters = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * 4));
+    L.sc.ts_step = static_cast<float *>(take(CISTA_V2E_MAX_BATCH * 4));
+    L.sc.meta = static_cast<int *>(take(16));
+    L.sc.nev = static_cast<unsigned long long *>(take(8));
+    L.vox_ws_bytes = cista_voxel_workspace_bytes(1, 0, B * nb, H, W);
+    L.vox_ws = take(L.vox_ws_bytes);
+    L.bytes = off;
+    return L;
+}
+
+inline dim3 g1d(long long n) { return dim3((unsigned)((n + 255) / 256)); }
+
+// torch.linspace(start, end, steps) in float32 (symmetric formula of ATen's linspace kernel)
+void linspace_f32(float start, float end, int steps, float *out) {
+    if (steps == 1) {
+        out[0] = start;
+        return;
+    }
+    const float step = (end - start) / (float)(steps - 1);
+    const int halfway = steps / 2;
+    for (int k = 0; k < steps; ++k)
+        out[k] = k < halfway ? start + step * (float)k : end - step * (float)(steps - k - 1);
+}
+
+}  // namespace cista_v2e
+
+using namespace cista_v2e;
+
+extern "C" {
+
+size_t cista_v2e_state_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return state_bytes(B, H, W);
+}
+
+size_t cista_v2e_workspace_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return carve_ws(nullptr, B, H, W, 16).bytes;   // sized for up to 16 bins
+}
+
+int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, void *state, const float *frames,
+                      const double *t_frames, int t_cols, int B, int F, int H, int W, float *voxels,
+                      unsigned long long *num_events, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!cfg || !hs || !state || !frames || !t_frames || !voxels || !workspace) return CISTA_ERR_INVALID;
+    if (B <= 0 || B > CISTA_V2E_MAX_BATCH || F < 2 || F > CISTA_V2E_MAX_FRAMES || H <= 0 || W <= 0)
+        return B > CISTA_V2E_MAX_BATCH || F > CISTA_V2E_MAX_FRAMES ? CISTA_ERR_UNSUPPORTED : CISTA_ERR_INVALID;
+    if (cfg->num_bins < 2 || cfg->num_bins > 16 || (t_cols != 2 && t_cols != F)) return CISTA_ERR_INVALID;
+    const WsLayout L = carve_ws(workspace, B, H, W, cfg->num_bins);
+    if (workspace_bytes < L.bytes) return CISTA_ERR_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const State s = carve_state(state, B, H, W);
+    const int nb = cfg->num_bins;
+
+    Call c;
+    memset(&c, 0, sizeof(c));
+    c.B = B; c.F = F; c.H = H; c.W = W; c.nb = nb;
+    c.cfg = *cfg;
+    c.seed = cfg->seed;
+    // frame times (:313-317): linspace over the first sample's first/last time, or its row
+    if (t_cols == 2) linspace_f32((float)t_frames[0], (float)t_frames[1], F, c.tf);
+    else
+        for (int k = 0; k < F; ++k) c.tf[k] = (float)t_frames[k];
+    const double duration = (double)(nb - 1) / (double)(F - 1);                    // :319
+    c.duration = (float)duration;
+    linspace_f32(0.0f, (float)(duration * (F - 1)), F, c.time_frames);            // :320
+    for (int b = 0; b < B; ++b) {                                                  // :322
+        const float span = (float)(t_frames[(size_t)b * t_cols + t_cols - 1] - t_frames[(size_t)b * t_cols]);
+        c.Tr[b] = (float)(nb - 1) * cfg->refractory_period_s * (1.0f / span);
+    }
+    const double pi2 = 3.14159265358979323846 * 2.0;
+    for (int k = 1; k < F; ++k) {
+        const float dt = c.tf[k] - c.tf[k - 1];                                    // :275
+        if (cfg->cutoff_hz > 0.0f) {
+            c.dt_lp0[k] = cfg->ql > 0.0f ? dt / (float)(1.0 / (pi2 * cfg->cutoff_hz * cfg->ql)) : 1.0f;
+            c.dt_lp1[k] = cfg->qs > 0.0f ? dt / (float)(1.0 / (pi2 * cfg->cutoff_hz * cfg->qs)) : 1.0f;
+        }
+    }
+    c.linlog_f = (1.0 / 20.0) * log(20.0);
+    const long long npx = (long long)B * H * W;
+
+    if (!hs->initialized) {
+        c.draw0 = hs->draw;
+        hipLaunchKernelGGL(v2e_init_kernel, g1d(npx), dim3(256), 0, st, c, s, frames);
+        hs->draw += 8;
+        hs->t_previous = (float)t_frames[0];
+        hs->initialized = 1;
+    } else if (cfg->refractory_period_s > 0.0f) {
+        hipLaunchKernelGGL(v2e_tmem_kernel, g1d(npx), dim3(256), 0, st, c, s);
+    }
+    if (!(c.tf[1] > hs->t_previous)) return CISTA_ERR_INVALID;                     // :339-342
+    if (hipMemsetAsync(voxels, 0, (size_t)B * nb * H * W * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+    if (hipMemsetAsync(L.sc.nev, 0, 8, st) != hipSuccess) return CISTA_ERR_HIP;
+    c.draw0 = hs->draw;
+    hs->draw += 2 * (unsigned long long)F + 16;
+    for (int n = 1; n < F; ++n) {
+        const float dt = c.tf[n] - hs->t_previous;                                 // :352
+        if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+        hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
+        hipLaunchKernelGGL(v2e_iters_kernel, dim3(1), dim3(64), 0, st, c, L.sc);
+        hipLaunchKernelGGL(v2e_emit_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, voxels, n, dt);
+        hs->t_previous = c.tf[n];                                                  // :518
+    }
+    if (num_events && hipMemcpyAsync(num_events, L.sc.nev, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
+        return CISTA_ERR_HIP;
+    if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
+    // event_preprocess_pytorch(mode='std', filter_hot_pixel=False) over the whole tensor (:526)
+    return cista_voxel_preprocess(voxels, 1, B * nb, H, W, CISTA_VOXEL_STD, 0.0f, L.vox_ws, L.vox_ws_bytes, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,131 @@
+"""Video-to-events emulator and the V2E2V pipeline on the GPU.
+
+``EventEmulator`` mirrors reference v2e/v2e_model.py:31-536 (same constructor arguments and
+defaults, ``reset()``, ``forward(frames, t_frames) -> (events, num_events)``) for
+``output_mode='voxel_grid'``, the mode V2E2VNet uses (model_v2e2v.py:28-29,46-61); the whole
+frame step runs in libcista_hip.so (include/cista_v2e.h).  ``V2E2VNet`` mirrors
+model_v2e2v.py:9-128: emulator + the drop-in CistaLSTCNet.
+
+Differences, by design: random draws come from a counter-based Philox stream keyed by ``seed``
+(statistically the reference's torch.normal / randn / rand, not the same numbers); ``seed=0``
+draws a fresh seed like the reference's unseeded torch RNG.  The raw-event output mode and the
+cv2 state display are not built (V2E2V never uses them).
+"""
+from __future__ import annotations
+
+import ctypes
+import random
+
+import numpy as np
+import torch
+
+from . import _lib
+from .e2v_model import CistaLSTCNet
+
+
+class CistaV2EConfig(ctypes.Structure):
+    _fields_ = [("num_bins", ctypes.c_int)] + [(n, ctypes.c_float) for n in (
+        "pl", "ps", "ql", "qs", "pos_thres", "neg_thres", "sigma_thres", "cutoff_hz", "leak_rate_hz",
+        "refractory_period_s", "shot_noise_rate_hz", "leak_jitter_fraction", "noise_rate_cov_decades")] + [
+        ("seed", ctypes.c_ulonglong)]
+
+
+class CistaV2EHostState(ctypes.Structure):
+    _fields_ = [("initialized", ctypes.c_int), ("t_previous", ctypes.c_float), ("draw", ctypes.c_ulonglong)]
+
+
+class EventEmulator(torch.nn.Module):
+    """v2e_model.py:31-156 constructor surface."""
+
+    def __init__(self, output_mode, pl=1, ps=1, ql=1, qs=1, num_bins=5, pos_thres=0.2, neg_thres=0.2,
+                 sigma_thres=0.03, cutoff_hz=0, leak_rate_hz=0.1, refractory_period_s=0, shot_noise_rate_hz=0,
+                 leak_jitter_fraction=0.1, noise_rate_cov_decades=0.1, seed=0, show_dvs_model_state=None,
+                 device="cuda"):
+        super().__init__()
+        if output_mode != "voxel_grid":
+            raise NotImplementedError("only output_mode='voxel_grid' (the V2E2V mode) is built")
+        if show_dvs_model_state:
+            raise NotImplementedError("the cv2 model-state display is not built")
+        self.output_mode = output_mode
+        self.num_bins = num_bins
+        self.device = torch.device(device)
+        self.cfg = CistaV2EConfig(num_bins, pl, ps, ql, qs, pos_thres, neg_thres, sigma_thres, cutoff_hz,
+                                  leak_rate_hz, refractory_period_s, shot_noise_rate_hz, leak_jitter_fraction,
+                                  noise_rate_cov_decades, seed if seed != 0 else random.getrandbits(63))
+        self.hs = CistaV2EHostState(0, 0.0, 0)
+        self.state = None
+        self.num_events = 0
+        self.frame_counter = 0
+        self._shape = None
+
+    def reset(self):
+        """v2e_model.py:255-263: the next forward re-initialises the base frame."""
+        self.hs.initialized = 0
+        self.frame_counter = 0
+
+    def forward(self, frames, t_frames):
+        """frames (B, F, H, W) intensities 0..255; t_frames (B, 2) or (B, F) seconds.
+        Returns (voxels (B, num_bins, H, W), num_events)."""
+        if not frames.is_cuda:
+            raise _lib.CistaError("the event emulator runs on a ROCm GPU only (no CPU fallback)")
+        B, F, H, W = frames.shape
+        self.frame_counter += F
+        fr = frames.detach().to(torch.float32).contiguous()
+        tf = np.ascontiguousarray(torch.as_tensor(t_frames).detach().cpu().to(torch.float64).numpy())
+        if tf.ndim != 2 or tf.shape[0] != B or tf.shape[1] not in (2, F):
+            raise ValueError("t_frames must be (batch, 2) or (batch, num_frames)")
+        L = _lib.lib()
+        if self.state is None or self._shape != (B, H, W) or self.state.device != fr.device:
+            self.state = torch.empty(L.cista_v2e_state_bytes(B, H, W), dtype=torch.uint8, device=fr.device)
+            self.ws = torch.empty(L.cista_v2e_workspace_bytes(B, H, W), dtype=torch.uint8, device=fr.device)
+            self._shape = (B, H, W)
+            self.hs.initialized = 0
+        out = torch.empty(B, self.num_bins, H, W, device=fr.device)
+        nev = torch.zeros(1, dtype=torch.int64, device=fr.device)
+        status = L.cista_v2e_forward(ctypes.byref(self.cfg), ctypes.byref(self.hs), self.state.data_ptr(),
+                                     fr.data_ptr(), tf.ctypes.data, tf.shape[1], B, F, H, W, out.data_ptr(),
+                                     nev.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
+                                     _lib.stream_handle(fr.device))
+        if status == 1 and self.hs.initialized:
+            raise ValueError("this frame time must be later than previous frame time")   # :339-342
+        _lib.check(status, "cista_v2e_forward")
+        self.num_events = int(nev.item())
+        return out, self.num_events
+
+
+class V2E2VNet(torch.nn.Module):
+    """model_v2e2v.py:9-128: EventEmulator (voxel grid) -> CistaLSTCNet."""
+
+    def __init__(self, cfgs, image_dim, device):
+        super().__init__()
+        self.height, self.width = image_dim
+        self.device = device
+        self.event_mode = cfgs.event_mode
+        self.num_bins = cfgs.num_bins
+        self.seq_id = -1
+        self.img_id = 0
+        self.num_events = -1
+        self.event_voxel_grids = None
+        self.v2e_net = EventEmulator(output_mode=self.event_mode, num_bins=cfgs.num_bins, pl=cfgs.pl, ps=cfgs.ps,
+                                     ql=cfgs.ql, qs=cfgs.qs, pos_thres=cfgs.C, neg_thres=cfgs.C,
+                                     sigma_thres=cfgs.threshold_sigma, cutoff_hz=cfgs.cutoff_hz,
+                                     refractory_period_s=cfgs.refractory_period_s, leak_rate_hz=0.1,
+                                     shot_noise_rate_hz=1, device=device)
+        self.e2v_net = CistaLSTCNet(image_dim=image_dim, base_channels=cfgs.base_channels, depth=cfgs.depth,
+                                    num_bins=cfgs.num_bins)
+
+    def reset_v2e(self, seq_idx):
+        if seq_idx != self.seq_id:
+            self.v2e_net.reset()
+            self.seq_id = seq_idx
+            self.img_id = 0
+
+    def forward(self, inputs, timestamps, pred_img, prev_states, seq_idx):
+        if pred_img is None:
+            pred_img = torch.zeros_like(inputs[:, 0:1, :, :]).float()
+        self.reset_v2e(seq_idx)
+        self.img_id += 1
+        voxels, n = self.v2e_net(inputs, timestamps)
+        self.num_events = n
+        self.event_voxel_grids = voxels.clone().detach()
+        return self.e2v_net(voxels, pred_img, prev_states)
