@@ -51,12 +51,87 @@ def parse():
                    help="frames of the bounded CPU-baseline sample (one sequence, B=1)")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--layer-reps", type=int, default=10)
-    p.add_argument("--mode", choices=["infer", "train"], default="infer",
-                   help="infer: the headline metric (config c2); train: BPTT step (configs c3/c4)")
+    p.add_argument("--mode", choices=["infer", "train", "v2e2v"], default="infer",
+                   help="infer: the headline metric (config c2); train: BPTT step (configs c3/c4); "
+                        "v2e2v: emulator + reconstruction at 720x1280 (config c5)")
+    p.add_argument("--pack-frames", type=int, default=10, help="v2e2v: frames per reconstruction")
     args = p.parse_args()
     if args.mode == "train" and "--batch" not in sys.argv:
         args.batch = 8            # BASELINE config c3: batch 8 per GPU (c4: 8 GPUs x 8 = 64)
+    if args.mode == "v2e2v":
+        if "--batch" not in sys.argv:
+            args.batch = 1        # config c5: one HFR video per GPU
+        if "--height" not in sys.argv:
+            args.height, args.width = 720, 1280
     return args
+
+
+def v2e2v_main(args, torch, vd, rank, world, device):
+    """Config c5 (model_v2e2v.py:72-128, test.py): per step, len_sequence reconstructions, each
+    from num_pack_frames high-frame-rate frames -> EventEmulator (voxel grid, V2E2VNet's noise
+    settings) -> CistaLSTCNet, states and prev image carried.  Replicas per GPU (independent
+    videos), frames/s = reconstructions of all ranks / max-over-ranks time."""
+    import types
+    from v2e2v_amd.v2e import V2E2VNet
+    B, L, H, W, P = args.batch, args.len_seq, args.height, args.width, args.pack_frames
+    cfgs = types.SimpleNamespace(event_mode="voxel_grid", num_bins=5, pl=1.0, ps=1.0, ql=1.0, qs=1.0, C=0.2,
+                                 threshold_sigma=0.03, cutoff_hz=30.0, refractory_period_s=0.001,
+                                 base_channels=64, depth=5)
+    net = V2E2VNet(cfgs, [H, W], device)
+    he_init_(torch, net.e2v_net, seed=7)
+    net = net.to(device).eval()
+    # synthetic HFR video resident in HBM: a textured background panning + a moving bright blob
+    g = torch.Generator(device=device).manual_seed(100 + rank)
+    yy, xx = torch.meshgrid(torch.arange(H, device=device, dtype=torch.float32),
+                            torch.arange(W, device=device, dtype=torch.float32), indexing="ij")
+    noise = torch.rand(B, 1, H, W, generator=g, device=device) * 4
+    n_frames = L * (P - 1) + 1
+    vid = torch.empty(n_frames, B, H, W, device=device)
+    for f in range(n_frames):
+        bg = 60 + 40 * torch.sin((xx + 2.0 * f) / 23.0) * torch.cos(yy / 31.0)
+        blob = 170 * torch.exp(-((xx - 100 - 6.0 * f) ** 2 + (yy - H / 2) ** 2) / 800.0)
+        vid[f] = (bg + blob + noise[:, 0]).clamp(0, 255)
+    dt = 1.0 / 240.0
+
+    def step(seq):
+        pred, states = None, None
+        for k in range(L):
+            frames = vid[k * (P - 1): k * (P - 1) + P].permute(1, 0, 2, 3).contiguous()
+            t0 = (seq * n_frames + k * (P - 1)) * dt
+            ts = (t0 + dt * torch.arange(P, dtype=torch.float64)).repeat(B, 1)
+            pred, states = net(frames, ts, pred, states, seq_idx=seq)
+        return pred
+
+    with torch.no_grad():
+        seq = 0
+        for _ in range(args.warmup):
+            step(seq)
+            seq += 1
+        torch.cuda.synchronize()
+        vd.barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            rec = step(seq)
+            seq += 1
+        torch.cuda.synchronize()
+        vd.barrier()
+        elapsed = vd.max_over_ranks(time.perf_counter() - t0, device)
+    frames_done = world * B * L * args.steps
+    if rank == 0:
+        print(json.dumps({
+            "metric": "V2E2V reconstructed frames/sec (v2e emulator + CISTA-LSTC) at 720x1280",
+            "value": round(frames_done / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "steps": args.steps, "warmup": args.warmup,
+            "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f32",
+            "data": "synthetic HFR video (panning texture + moving blob), random-init weights",
+            "config": {"workload": f"V2E2V {H}x{W}, num_pack_frames={P}, len_sequence={L}, {B} video/GPU",
+                       "batch_per_gpu": B, "len_sequence": L, "num_pack_frames": P,
+                       "parallelism": f"replicas x{world}"},
+            "events_last_pack": int(net.num_events), "outputs_finite": bool(torch.isfinite(rec).all())}),
+            flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
 
 
 def train_main(args, torch, vd, rank, world, device):
@@ -301,6 +376,8 @@ def main():
     vd.init("nccl", device)
     if args.mode == "train":
         return train_main(args, torch, vd, rank, world, device)
+    if args.mode == "v2e2v":
+        return v2e2v_main(args, torch, vd, rank, world, device)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
 
     model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)

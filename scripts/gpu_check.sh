@@ -25,6 +25,9 @@ for step in "$@"; do
     tbench)
       timeout -k 10 600 python bench.py --mode train ${TBENCH_ARGS:---steps 3 --warmup 1} > gpurun_out/tbench.json 2> gpurun_out/tbench.err
       rc=$?; echo "tbench rc=$rc"; cat gpurun_out/tbench.json; tail -3 gpurun_out/tbench.err; [ $rc -eq 0 ] || exit $rc ;;
+    vbench)
+      timeout -k 10 600 python bench.py --mode v2e2v ${VBENCH_ARGS:---steps 2 --warmup 1} > gpurun_out/vbench.json 2> gpurun_out/vbench.err
+      rc=$?; echo "vbench rc=$rc"; cat gpurun_out/vbench.json; tail -3 gpurun_out/vbench.err; [ $rc -eq 0 ] || exit $rc ;;
     tprof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/proft -o run -- python3 bench.py --mode train --steps 1 --warmup 1 > gpurun_out/proft_bench.json 2> gpurun_out/proft.err
