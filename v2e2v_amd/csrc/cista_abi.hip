@@ -177,7 +177,11 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     a.tiles_x = t.tx;
     constexpr int nblk_cols = WN * NW * 16;
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI>;
+    // the training variant (SV) only for epilogues that save activations, and only when asked
+    constexpr bool HAS_SV = EPI == EPI_ISTA_P || EPI == EPI_LSTC_CELL || EPI == EPI_LSTC_OUT || EPI == EPI_LSTM;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false>;
+    if constexpr (HAS_SV)
+        if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr) kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
     // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))

@@ -340,7 +340,9 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
 // The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
 // MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
 // ------------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0>
+// SV: training variant -- the epilogue also stores the activations the BPTT backward needs
+// (out1 / out2, see ConvArgs); the inference variant has no such stores in its epilogue.
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false>
 __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     // NI > 0: double-buffered K loop (two LDS images, next chunk's loads in NI x 8 VGPRs)
     static_assert(WM * WN == 4, "4 waves per workgroup");
@@ -627,8 +629,15 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
             const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
             const unsigned o = (unsigned)(off < 0 ? 0 : off) + (unsigned)ch;
             A0[it] = A1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if constexpr (USE_A0)
-                if (a.aux0) A0[it] = *(const float4 *)(a.aux0 + o);
+            if constexpr (USE_A0) {
+                // branch-free: a NULL aux0 (a None state) reads out0 instead and is zeroed by a
+                // select; a branch here makes the compiler drain vmcnt at the join (no prefetch)
+                // aux0 may be NULL only where it is a previous state (c_prev of LSTC / LSTM)
+                const bool has = (EPI != EPI_LSTC_CELL && EPI != EPI_LSTM) || a.aux0 != nullptr;
+                const float *src = has ? a.aux0 : a.out0;          // out0: same layout, valid memory
+                const float4 v = *(const float4 *)(src + o);
+                A0[it] = has ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+            }
             if constexpr (USE_A1) A1[it] = *(const float4 *)(a.aux1 + o);
         }
     };
@@ -636,24 +645,34 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     load_aux(0, curA0, curA1);
     // results are kept in registers (acc[m]'s registers die as res[m] is born) and stored in
     // one burst after the last aux load: no load then waits behind an outstanding store
-    float4 res[MT_W][NIT];
+    // the LSTC epilogues (long-K gates convs, MT_W = 12) store in the loop instead: their
+    // result registers would not fit next to the accumulators without spilling
+    constexpr bool BURST = EPI != EPI_LSTC_CELL && EPI != EPI_LSTC_OUT;
+    float4 res[BURST ? MT_W : 1][NIT];
+    float4 res1[EPI == EPI_LSTM ? MT_W : 1][NIT];         // EPI_LSTM: the cell state c (out1)
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
         float4 nxtA0[NIT], nxtA1[NIT];
+        // compiler-only barrier: keeps the prefetch exactly one m-tile ahead (hoisting every
+        // m-tile's loads to the top costs MT_W x NIT x 4 VGPRs and spills)
+        asm volatile("" ::: "memory");
         if (m + 1 < MT_W) load_aux(m + 1, nxtA0, nxtA1);
 #pragma unroll
         for (int n = 0; n < NW; ++n)
 #pragma unroll
             for (int j = 0; j < 4; ++j) T[(4 * grp + j) * LDT + n * 16 + col] = acc[m][n][j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 #pragma unroll
         for (int it0 = 0; it0 < 16 * CG; it0 += 64) {
             {
                 const int row = (it0 + lane) / CG;
-                const int off = ptab[(wm * MT_W + m) * 16 + row];
-                if (off >= 0) {
+                // items outside the image compute on a clamped (valid) offset and are only skipped
+                // by the stores: no divergent branch, so no vmcnt drain at a join point
+                const int off_raw = ptab[(wm * MT_W + m) * 16 + row];
+                const int off = off_raw < 0 ? 0 : off_raw;
+                {
                     float4 v[G];
 #pragma unroll
                     for (int g = 0; g < G; ++g) {
@@ -682,7 +701,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             r1[e] = x;
                             r[e] = fmaxf(x - ll[e], 0.0f) - fmaxf(-x - ll[e], 0.0f);
                         }
-                        if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+                        if constexpr (SV)
+                            if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_OUT) {
                         const float4 c = curA0[it0 / 64];
                         const float *cc = reinterpret_cast<const float *>(&c);
@@ -691,7 +711,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             r1[e] = sigmoidf_(vv[e]);
                             r[e] = r1[e] * tanhf(cc[e]);
                         }
-                        if (a.out1) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+                        if constexpr (SV)
+                            if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
                     } else if constexpr (EPI == EPI_LSTC_CELL) {
                         // packed n-tile order per channel block: (in, forget)
                         const float4 z0 = curA1[it0 / 64];
@@ -705,7 +726,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             sf[e] = sigmoidf_(vv[4 + e]);
                             r[e] = sf[e] * pp[e] + si[e] * zz[e];
                         }
-                        if (a.out1) {
+                        if (SV && off_raw >= 0) {
                             *(float4 *)(a.out1 + o) = make_float4(si[0], si[1], si[2], si[3]);
                             *(float4 *)(a.out2 + o) = make_float4(sf[0], sf[1], sf[2], sf[3]);
                         }
@@ -724,8 +745,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             r1[e] = c;
                             r[e] = go[e] * tanhf(c);
                         }
-                        *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
-                        if (a.out2) {
+                        res1[m][it0 / 64] = make_float4(r1[0], r1[1], r1[2], r1[3]);   // c, stored in the burst
+                        if (SV && off_raw >= 0) {
                             float *gsv = a.out2 + 4u * (unsigned)off + (unsigned)ch;
                             *(float4 *)(gsv) = make_float4(gi[0], gi[1], gi[2], gi[3]);
                             *(float4 *)(gsv + a.Cout) = make_float4(gr[0], gr[1], gr[2], gr[3]);
@@ -733,7 +754,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                             *(float4 *)(gsv + 3 * a.Cout) = make_float4(gg[0], gg[1], gg[2], gg[3]);
                         }
                     }
-                    res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
+                    if constexpr (BURST) res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
+                    else if (off_raw >= 0) *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
                 }
             }
         }
@@ -744,17 +766,20 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                 curA1[it] = nxtA1[it];
             }
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
         __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
+    if constexpr (BURST)
 #pragma unroll
     for (int m = 0; m < MT_W; ++m)
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
             const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
-            if (off >= 0 && (CISTA_EXP_NOEPI == 0 || res[m][it].x == 12345.f))
+            if (off >= 0 && (CISTA_EXP_NOEPI == 0 || res[m][it].x == 12345.f)) {
                 *(float4 *)(a.out0 + (unsigned)off + (unsigned)ch) = res[m][it];
+                if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
+            }
         }
 }
 
