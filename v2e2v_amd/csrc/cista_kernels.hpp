@@ -38,6 +38,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 //   CISTA_EXP_NOA      one A fragment per tap reused for every m-tile (no per-m LDS reads)
 //   CISTA_EXP_NOSTAGE  halo staged only for the first K-chunk
 //   CISTA_EXP_NOEPI    epilogue stores skipped
+//   CISTA_EXP_SMALLSTORE  epilogue stores wrapped into a window of (mask + 1) floats
 #ifndef CISTA_EXP_NOB
 #define CISTA_EXP_NOB 0
 #endif
@@ -49,6 +50,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #endif
 #ifndef CISTA_EXP_NOEPI
 #define CISTA_EXP_NOEPI 0
+#endif
+#ifndef CISTA_EXP_SMALLSTORE
+#define CISTA_EXP_SMALLSTORE 0     // != 0: store offsets masked into a small window (value = mask)
 #endif
 
 
@@ -755,7 +759,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         }
                     }
                     if constexpr (BURST) res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
+#if CISTA_EXP_SMALLSTORE
+                    else if (off_raw >= 0) *(float4 *)(a.out0 + (o & (unsigned)CISTA_EXP_SMALLSTORE)) = make_float4(r[0], r[1], r[2], r[3]);
+#else
                     else if (off_raw >= 0) *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
+#endif
                 }
             }
         }
@@ -777,7 +785,11 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         for (int it = 0; it < NIT; ++it) {
             const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
             if (off >= 0 && (CISTA_EXP_NOEPI == 0 || res[m][it].x == 12345.f)) {
+#if CISTA_EXP_SMALLSTORE
+                *(float4 *)(a.out0 + (((unsigned)off + (unsigned)ch) & (unsigned)CISTA_EXP_SMALLSTORE)) = res[m][it];
+#else
                 *(float4 *)(a.out0 + (unsigned)off + (unsigned)ch) = res[m][it];
+#endif
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
             }
         }
