@@ -32,6 +32,15 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/proft -o run -- python3 bench.py --mode train --steps 1 --warmup 1 > gpurun_out/proft_bench.json 2> gpurun_out/proft.err
       rc=$?; echo "tprof rc=$rc"; tail -3 gpurun_out/proft.err; [ $rc -eq 0 ] || exit $rc ;;
+    vtests)
+      # persistent-loop parity of every variant build (bit-exact batch vs single runs)
+      for f in v2e2v_amd/variants/*.so; do
+        CISTA_HIP_LIB=$f timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -p no:cacheprovider -k "persistent or f3 or stage" > gpurun_out/vtests_$(basename $f .so).log 2>&1
+        rc=$?; echo "vtests $(basename $f) rc=$rc"; tail -1 gpurun_out/vtests_$(basename $f .so).log; ok $rc || exit $rc
+      done ;;
+    ab)
+      timeout -k 10 900 bash scripts/ab_layers.sh ${AB_B:-64}
+      rc=$?; echo "ab rc=$rc"; cat gpurun_out/layers.jsonl; [ $rc -eq 0 ] || exit $rc ;;
     list)
       timeout -k 10 120 rocprofv3 -L > gpurun_out/counters.txt 2>&1; echo "list rc=$?" ;;
     sq)

@@ -242,6 +242,27 @@ def test_alias_and_shape_errors():
     assert st == 5   # CISTA_ERR_ALIAS
 
 
+def test_batch_equals_single_two_frames():
+    """At B=12, 180x240 (720 workgroups per 128-column conv, more than are resident at once)
+    every sample must equal its own B=1 run bit for bit, states included, over two recurrent
+    frames: no cross-sample coupling anywhere in the frame schedule."""
+    params = fx.stress_params(64, 5, 5, seed=21)
+    m = make_model(params=params)
+    B = 12
+    rng = np.random.default_rng(5)
+    vox = gpu(rng.standard_normal((2, B, 5, 180, 240)).astype(np.float32))
+    prev = torch.rand(B, 1, 180, 240, device=DEV)
+    with torch.no_grad():
+        r, s = m(vox[0], prev, None)
+        r, s = m(vox[1], r, s)
+        for i in (0, 5, 11):
+            ri, si = m(vox[0, i:i + 1], prev[i:i + 1], None)
+            ri, si = m(vox[1, i:i + 1], ri, si)
+            assert torch.equal(r[i:i + 1], ri), i
+            assert torch.equal(s[0][i:i + 1], si[0]) and torch.equal(s[1][i:i + 1], si[1]), i
+            assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
+
+
 def test_determinism_and_batch_independence():
     """Size-independent properties at the bench size: bit-identical re-runs, and sample i of a
     batched launch equals the same sample run alone (no cross-sample coupling)."""

@@ -125,6 +125,7 @@ struct WgradArgs {
                                         // produced by the ci-block-0 workgroups
     int vec4;                           // float4 staging: Gc, Goff, x0c, x1c, Cin % 4 == 0, NHWC
                                         // input, tile <= 16x16 (S1/UP) or 8x8 (S2)
+    const float *gscale;                // wgrad_split_kernel: {s, 1/s} power-of-two scale of G
 };
 
 typedef float f32x4w __attribute__((ext_vector_type(4)));
@@ -341,6 +342,188 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 #pragma unroll
             for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[t][j];
     }
+}
+
+// --------------------------------------------------------------------------------------------
+// wgrad on split-f16 MFMA (v_mfma_f32_16x16x32_f16, 3 passes hi*hi + hi*lo + lo*hi, fp32
+// accumulate) for the stride-1 NHWC convs (XS_S1, 64-aligned Cout, 32-aligned Cin):
+//   dW[co][ci][t] = sum_P G(P, co) * Xpad(P + t, ci)  =  per tap a (co x ci) GEMM, K = pixels.
+// Workgroup = 64 co x 32 ci block; 4 waves = 2 (32 co) x 2 (16 ci), 2 x 9 accumulators each.
+// Pixel tile 6 x 16 = 96 = 3 K-steps of 32; a lane's 8 K values are 8 consecutive pixels of
+// one row.  LDS (fp16, hi and lo planes):
+//   Gs[part][co][GST]           output gradient, pre-scaled by the per-tensor power of two
+//                               gscale[0] so its fp16 split keeps fp32 accuracy;
+//   Xs[part][dx][ci][XST]       the reflect-padded input halo (8 rows x 18 cols) as three
+//                               column-shifted 8 x 16 copies (dx = 0, 1, 2), so that every
+//                               tap's B fragment is one aligned ds_read_b128.
+// Row strides GST = 104 and XST = 136 halves put the 16 lanes of a fragment read on 16
+// distinct 16-byte bank groups.  X needs no scale: it is a forward conv input, already bound
+// by the forward's split to |x| < 65504.  Per-split partials as wgrad_kernel (same reduce).
+// --------------------------------------------------------------------------------------------
+constexpr int WS_TH = 6, WS_TW = 16, WS_NPX = 96, WS_HH = 8, WS_HW = 18;
+constexpr int WS_GST = WS_NPX + 8;                  // halves per co row
+constexpr int WS_XST = WS_HH * WS_TW + 8;           // halves per (dx, ci) plane
+constexpr size_t WS_LDS = (size_t)2 * 64 * WS_GST * 2 + (size_t)2 * 3 * 32 * WS_XST * 2;
+
+__device__ __forceinline__ void split_pack8(const float (&v)[8], u32x4 &hi, u32x4 &lo) {
+    f16x8 h, l;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+        const _Float16 hb = (_Float16)v[i];
+        h[i] = hb;
+        l[i] = (_Float16)(v[i] - (float)hb);
+    }
+    hi = __builtin_bit_cast(u32x4, h);
+    lo = __builtin_bit_cast(u32x4, l);
+}
+
+__global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) {
+    extern __shared__ u32x4 wsm4[];
+    _Float16 *Gs = reinterpret_cast<_Float16 *>(wsm4);           // [2][64][GST]
+    _Float16 *Xs = Gs + 2 * 64 * WS_GST;                          // [2][3][32][XST]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nci = a.Cin / 32;
+    const int co0 = (blockIdx.x / nci) * 64, ci0 = (blockIdx.x % nci) * 32;
+    const int wco = (wave >> 1) * 32, wci = (wave & 1) * 16;
+    const float gsc = a.gscale[0];
+    f32x4 acc[2][9];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = a.bpartial && (blockIdx.x % nci) == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    // staging items: G (tid < 192): co quad cq = tid & 15, pixel group pg = tid >> 4 (8 px);
+    //                X (tid < 128): ci quad xq = tid & 7, halo row r = (tid >> 3) & 7, column
+    //                group cg = tid >> 6 (halo columns 8 cg .. 8 cg + 9)
+    const int cq = tid & 15, pg = tid >> 4;
+    const int xq = tid & 7, xr = (tid >> 3) & 7, xcg = (tid >> 6) & 1;
+    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * WS_TH, ox0 = tx * WS_TW;
+        // global loads of both operands first (latency overlap), then split + LDS stores
+        float4 gv[8], xv[10];
+        if (tid < 192) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                const int p = pg * 8 + j;
+                const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+                gv[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (oy < a.Hout && ox < a.Wout)
+                    gv[j] = *reinterpret_cast<const float4 *>(
+                        a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 4 * cq);
+            }
+        }
+        if (tid < 128) {
+#pragma unroll
+            for (int j = 0; j < 10; ++j)
+                xv[j] = wg_load_x4<XS_S1>(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 4 * xq);
+        }
+        __syncthreads();                       // the previous tile's fragment reads are done
+        if (tid < 192) {
+            if (do_bias) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    bsum.x += gv[j].x; bsum.y += gv[j].y; bsum.z += gv[j].z; bsum.w += gv[j].w;
+                }
+            }
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float v[8];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) v[j] = (&gv[j].x)[c] * gsc;    // exact: power of two
+                u32x4 hi, lo;
+                split_pack8(v, hi, lo);
+                const int row = 4 * cq + c;
+                *reinterpret_cast<u32x4 *>(Gs + row * WS_GST + pg * 8) = hi;
+                *reinterpret_cast<u32x4 *>(Gs + (64 + row) * WS_GST + pg * 8) = lo;
+            }
+        }
+        if (tid < 128) {
+#pragma unroll
+            for (int c = 0; c < 4; ++c) {
+                float hs[10], ls[10];
+#pragma unroll
+                for (int j = 0; j < 10; ++j) {
+                    const float x = (&xv[j].x)[c];
+                    const _Float16 hb = (_Float16)x;
+                    hs[j] = (float)hb;
+                    ls[j] = x - hs[j];
+                }
+#pragma unroll
+                for (int dx = 0; dx < 3; ++dx) {
+                    f16x8 h, l;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) {
+                        h[j] = (_Float16)hs[j + dx];
+                        l[j] = (_Float16)ls[j + dx];
+                    }
+                    const int plane = dx * 32 + 4 * xq + c;
+                    _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * xcg;
+                    *reinterpret_cast<u32x4 *>(d) = __builtin_bit_cast(u32x4, h);
+                    *reinterpret_cast<u32x4 *>(d + 3 * 32 * WS_XST) = __builtin_bit_cast(u32x4, l);
+                }
+            }
+        }
+        __syncthreads();
+        const int kg = lane >> 4, r16 = lane & 15;
+#pragma unroll
+        for (int s = 0; s < WS_NPX / 32; ++s) {
+            const int p0 = 32 * s + 8 * kg;
+            const int py = p0 >> 4, px0 = p0 & 15;
+            u32x4 ah[2], al[2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int row = wco + 16 * u + r16;
+                ah[u] = *reinterpret_cast<const u32x4 *>(Gs + row * WS_GST + p0);
+                al[u] = *reinterpret_cast<const u32x4 *>(Gs + (64 + row) * WS_GST + p0);
+            }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int dy = t / 3, dx = t % 3;
+                const _Float16 *src = Xs + (dx * 32 + wci + r16) * WS_XST + (py + dy) * WS_TW + px0;
+                const f16x8 bh = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4 *>(src));
+                const f16x8 bl = __builtin_bit_cast(f16x8, *reinterpret_cast<const u32x4 *>(src + 3 * 32 * WS_XST));
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const f16x8 xh = __builtin_bit_cast(f16x8, ah[u]);
+                    const f16x8 xl = __builtin_bit_cast(f16x8, al[u]);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bh, acc[u][t], 0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, bl, acc[u][t], 0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, bh, acc[u][t], 0, 0, 0);
+                }
+            }
+        }
+    }
+    if (do_bias) {
+        // per-thread partial sums of 4 co over its pixel groups -> co sums in a fixed order
+        __syncthreads();
+        float4 *red = reinterpret_cast<float4 *>(wsm4);
+        if (tid < 192) red[tid] = bsum;
+        __syncthreads();
+        if (tid < 64) {
+            float t = 0.0f;
+            for (int k = 0; k < 12; ++k) t += (&red[k * 16 + (tid >> 2)].x)[tid & 3];
+            a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + tid] = t;
+        }
+    }
+    // acc[u][t][j]: row (cout) wco + 16u + 4*(lane>>4) + j, col (cin) wci + (lane & 15)
+    const float inv = a.gscale[1];
+    float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            const int co = co0 + wco + 16 * u + 4 * (lane >> 4) + j;
+            const int ci = ci0 + wci + (lane & 15);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[u][t][j] * inv;
+        }
 }
 
 // dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9)
