@@ -576,17 +576,80 @@ struct Bwd {
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
 
+// per-tensor power-of-two scale {s, 1/s} of an output gradient G (n floats) for its fp16
+// splits (split-f16 dgrad and wgrad), in a rotating slot of the backward workspace
+const float *grad_scale(Bwd &k, const float *G, long n) {
+    unsigned *am = k.ws.amax + (k.slot & 7);
+    float *sc = k.ws.scl + 2 * (k.slot & 7);
+    ++k.slot;
+    if (hipMemsetAsync(am, 0, 4, k.st) != hipSuccess) return nullptr;
+    hipLaunchKernelGGL(absmax_kernel, dim3(512), dim3(256), 0, k.st, G, n, am);
+    hipLaunchKernelGGL(scale_from_amax_kernel, dim3(1), dim3(1), 0, k.st, (const unsigned *)am, sc);
+    return sc;
+}
+
+#ifndef CISTA_WGRAD_SPLIT
+#define CISTA_WGRAD_SPLIT 1   // 0: every wgrad on the exact fp32-MFMA kernel (A/B builds)
+#endif
+
 // dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor; and, when
-// db != NULL, db (+)= sign * (pixel sum of G) from the same pass over G (bias gradient)
+// db != NULL, db (+)= sign * (pixel sum of G) from the same pass over G (bias gradient).
+// gsc (the grad_scale of G) selects the split-f16 kernel where the shape allows it.
 template <int XS>
 int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, int x0c,
           const float *X1, int x1c, int Cin, int Hin, int Win, int Hout, int Wout, float *dst,
-          float sign, int accumulate, float *db) {
+          float sign, int accumulate, float *db, const float *gsc = nullptr) {
     WgradArgs a;
     memset(&a, 0, sizeof(a));
     a.G = G; a.Gc = Gc; a.Goff = Goff;
     a.X0 = X0; a.x0c = x0c; a.X1 = X1; a.x1c = x1c;
     a.B = k.B; a.Hin = Hin; a.Win = Win; a.Hout = Hout; a.Wout = Wout;
+    a.Cout = Cout; a.Cin = Cin;
+    a.partial = k.ws.part;
+    a.bpartial = db ? k.ws.bpart : nullptr;
+    if (CISTA_WGRAD_SPLIT && XS == XS_S1 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 &&
+        Goff % 4 == 0 && x0c % 32 == 0 && x1c % 32 == 0 && Hin == Hout && Win == Wout) {
+        a.gscale = gsc;
+        a.TH = WS_TH; a.TW = WS_TW;
+        a.tiles_y = (Hout + WS_TH - 1) / WS_TH;
+        a.tiles_x = (Wout + WS_TW - 1) / WS_TW;
+        const int nblk = (Cout / 64) * (Cin / 32);
+        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        int ns = (WG_BLOCKS / 2) / nblk;   // partials: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9
+        ns = ns > ntiles ? ntiles : ns;
+        ns = ns < 1 ? 1 : ns;
+        ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
+        a.nsplit = ns;
+        if (!allow_big_lds((const void *)wgrad_split_kernel)) return CISTA_ERR_HIP;
+        hipLaunchKernelGGL(wgrad_split_kernel, dim3(nblk, ns), dim3(256), WS_LDS, k.st, a);
+        const long n = (long)Cout * Cin * 9;
+        hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
+                           dst, sign, accumulate);
+        if (db)
+            hipLaunchKernelGGL(reduce_partials_kernel, g1d(Cout), dim3(256), 0, k.st, (const float *)k.ws.bpart,
+                               ns, (long)Cout, db, sign, accumulate);
+        return hip_ok();
+    }
+    if (XS == XS_S1 && Cout == 1 && Gc == 1 && Goff == 0 && Cin % 32 == 0 && x0c % 4 == 0 && x1c % 4 == 0 &&
+        Hin == Hout && Win == Wout) {                        // final_conv: VALU, one output row
+        a.TH = 16; a.TW = 16;
+        a.tiles_y = (Hout + 15) / 16;
+        a.tiles_x = (Wout + 15) / 16;
+        const int ncb = Cin / 32;
+        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        int ns = 512 / ncb;
+        ns = ns > ntiles ? ntiles : ns;
+        ns = ns < 1 ? 1 : ns;
+        a.nsplit = ns;
+        hipLaunchKernelGGL(wgrad_c1_kernel, dim3(ncb, ns), dim3(256), 0, k.st, a);
+        const long n = (long)Cin * 9;
+        hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
+                           dst, sign, accumulate);
+        if (db)
+            hipLaunchKernelGGL(reduce_partials_kernel, g1d(1), dim3(256), 0, k.st, (const float *)k.ws.bpart, ns,
+                               1L, db, sign, accumulate);
+        return hip_ok();
+    }
     const int T = XS == XS_S2 ? 8 : 16;
     a.TH = Hout < T ? Hout : T;
     a.TW = Wout < T ? Wout : T;
@@ -629,16 +692,12 @@ int dgrad_vec(Bwd &k, const DgradSmallArgs &d, const float *Wref) {
 }
 
 // dxp (B, h+2, w+2, N) = padded-domain gradient of conv `id`'s input, from G (B,h,w,K)
-int dgrad_conv(Bwd &k, int id, const float *G, float *dxp) {
+// sc: grad_scale of G (computed here when NULL)
+int dgrad_conv(Bwd &k, int id, const float *G, float *dxp, const float *sc = nullptr) {
     const ConvShape s = conv_shape(id, k.C);
     const int Hin = id == CV_UP ? k.H : k.h, Win = id == CV_UP ? k.W : k.w;
-    const long n = (long)k.B * Hin * Win * s.cout;
-    unsigned *am = k.ws.amax + (k.slot & 7);
-    float *sc = k.ws.scl + 2 * (k.slot & 7);
-    ++k.slot;
-    if (hipMemsetAsync(am, 0, 4, k.st) != hipSuccess) return CISTA_ERR_HIP;
-    hipLaunchKernelGGL(absmax_kernel, dim3(512), dim3(256), 0, k.st, G, n, am);
-    hipLaunchKernelGGL(scale_from_amax_kernel, dim3(1), dim3(1), 0, k.st, (const unsigned *)am, sc);
+    if (!sc) sc = grad_scale(k, G, (long)k.B * Hin * Win * s.cout);
+    if (!sc) return CISTA_ERR_HIP;
     ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in0 = G; a.c0 = s.cout; a.in1 = nullptr; a.c1 = 0;
@@ -698,13 +757,15 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     // ---- 3. ConvLSTM ---------------------------------------------------------------------
     hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C);
-    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b));
-    CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp));
+    const float *gsc = grad_scale(k, ws.Gl, hw * 4 * C);
+    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
+    CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y));        // relu(Dg) mask
     if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
-    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b));
-    CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp));
+    gsc = grad_scale(k, ws.gy, hw * C);
+    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
+    CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
     CHECK(copy_or_zero(ws.gz, g.g_z, (size_t)hw * 2 * C, st));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
     // ---- 5. ISTA, reversed (tied D, P, lambda accumulate over iterations) -------------------
@@ -732,13 +793,15 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                            lam, ws.gv, ws.dlp, hw, 2 * C);
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
-        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b));
-        CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp));
+        gsc = grad_scale(k, ws.gv, hw * 2 * C);
+        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b, gsc));
+        CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr));
         CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
-        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b));
-        CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp));
+        gsc = grad_scale(k, ws.gxk, hw * C);
+        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b, gsc));
+        CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp, gsc));
         CHECK(copy_or_zero(ws.gz, ws.gv, (size_t)hw * 2 * C, st));          // identity path
         CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 1, nullptr));
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
@@ -751,19 +814,22 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C);
+    gsc = grad_scale(k, ws.Go, hw * 2 * C);
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
-                       pg.out_gates_w, 1.0f, 0, pg.out_gates_b));
-    CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp));
+                       pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
+    CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
+    gsc = grad_scale(k, ws.Gl, hw * 4 * C);
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
-                       pg.gates_w, 1.0f, 0, pg.gates_b));
-    CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp));
+                       pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
+    CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
-    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b));
-    CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp));
+    gsc = grad_scale(k, ws.gz0, hw * 2 * C);
+    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
+    CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
     float *xfull = ws.gU, *gxfull = ws.gU;   // x_full is dead once W0's wgrad has run

@@ -526,6 +526,71 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
         }
 }
 
+// --------------------------------------------------------------------------------------------
+// wgrad of a one-output-channel stride-1 conv (final_conv, 64 -> 1): dW[ci][t] = sum_P g(P) *
+// Xpad(P + t, ci) on VALU (an MFMA block would waste 31 of 32 rows).  blockIdx.x = 32-channel
+// block, blockIdx.y = split over 16 x 16 pixel tiles.  The reflect-padded 18 x 18 x 32 input
+// halo sits in LDS (row stride 33: conflict-free); thread = (channel tid & 31, pixel phase
+// tid >> 5) accumulates 9 taps over its phase's pixels; phases are summed in a fixed order.
+// --------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void wgrad_c1_kernel(const WgradArgs a) {
+    __shared__ float Xs[18 * 18 * 33];
+    __shared__ float gs[256];
+    __shared__ float red[8][32 * 9 + 1];
+    const int tid = threadIdx.x, ci = tid & 31, ph = tid >> 5;
+    const int ci0 = blockIdx.x * 32;
+    float acc[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) acc[t] = 0.0f;
+    float bsum = 0.0f;
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * 16, ox0 = tx * 16;
+        __syncthreads();
+        {
+            const int oy = oy0 + (tid >> 4), ox = ox0 + (tid & 15);
+            gs[tid] = (oy < a.Hout && ox < a.Wout)
+                          ? a.G[((size_t)b * a.Hout + oy) * a.Wout + ox] : 0.0f;
+        }
+        for (int i = tid; i < 18 * 18 * 8; i += 256) {          // 8 channel quads per pixel
+            const int hp = i >> 3, q = i & 7;
+            const int hy = hp / 18, hx = hp - hy * 18;
+            const float4 v = wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 4 * q);
+            float *d = Xs + hp * 33 + 4 * q;
+            d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
+        }
+        __syncthreads();
+        for (int p = ph; p < 256; p += 8) {
+            const float g = gs[p];
+            if (blockIdx.x == 0 && ci == 0) bsum += g;
+            const int hb = (p >> 4) * 18 + (p & 15);
+#pragma unroll
+            for (int t = 0; t < 9; ++t) acc[t] = fmaf(g, Xs[(hb + (t / 3) * 18 + (t % 3)) * 33 + ci], acc[t]);
+        }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < 9; ++t) red[ph][ci * 9 + t] = acc[t];
+    if (ci == 0) red[ph][32 * 9] = bsum;
+    __syncthreads();
+    float *part = a.partial + (size_t)blockIdx.y * a.Cin * 9;
+    for (int i = tid; i < 32 * 9; i += 256) {
+        float s = 0.0f;
+        for (int k = 0; k < 8; ++k) s += red[k][i];
+        if (ci0 + i / 9 < a.Cin) part[ci0 * 9 + i] = s;
+    }
+    if (blockIdx.x == 0 && tid == 0 && a.bpartial) {
+        float s = 0.0f;
+        for (int k = 0; k < 8; ++k) s += red[k][32 * 9];
+        a.bpartial[blockIdx.y] = s;
+    }
+}
+
 // dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9)
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *partial, int nsplit, long n,
                                                               float *dst, float sign, int accumulate) {

@@ -539,6 +539,13 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         float bz[NW];
 #pragma unroll
         for (int n = 0; n < NW; ++n) bz[n] = a.bias[(nt0 + n) * 16 + col];
+        // final_conv's [tap][C] weights staged once in LDS: read from global inside the loop
+        // they would be re-fetched after every store (the stores may alias them), each fetch
+        // waiting behind the stores before it (vmcnt is in order)
+        __syncthreads();                                   // the last chunk's A reads are done
+        float *wfs = reinterpret_cast<float *>(smem);
+        for (int i = threadIdx.x; i < 9 * a.Cout; i += 256) wfs[i] = a.aux0[i];
+        __syncthreads();
 #pragma unroll
         for (int m = 0; m < MT_W; ++m) {
             float v[48];
@@ -546,7 +553,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
             for (int i = 0; i < 48; ++i) v[i] = 0.0f;
 #pragma unroll
             for (int n = 0; n < NW; ++n) {
-                const float *wf = a.aux0 + (nt0 + n) * 16 + col;
+                const float *wf = wfs + (nt0 + n) * 16 + col;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float u = fmaxf(acc[m][n][j] + bz[n], 0.0f);
