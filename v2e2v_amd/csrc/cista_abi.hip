@@ -630,6 +630,27 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
                                ns, (long)Cout, db, sign, accumulate);
         return hip_ok();
     }
+    if (XS == XS_NCHW && Cout <= 32 && Cin == x0c && Cin >= 1 && Cin <= 8 && !X1 && Hin == Hout && Win == Wout) {
+        a.TH = 16; a.TW = 16;                                // We / Wi: VALU over NCHW planes
+        a.tiles_y = (Hout + 15) / 16;
+        a.tiles_x = (Wout + 15) / 16;
+        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        const int ns = ntiles < 512 ? ntiles : 512;
+        a.nsplit = ns;
+        switch (Cin) {
+#define WSCASE(n) \
+    case n: hipLaunchKernelGGL(wgrad_small_kernel<n>, dim3(ns), dim3(256), 0, k.st, a); break;
+            WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6) WSCASE(7) WSCASE(8)
+#undef WSCASE
+        }
+        const long n = (long)Cout * Cin * 9;
+        hipLaunchKernelGGL(reduce_partials_kernel, g1d(n), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
+                           dst, sign, accumulate);
+        if (db)
+            hipLaunchKernelGGL(reduce_partials_kernel, g1d(Cout), dim3(256), 0, k.st, (const float *)k.ws.bpart, ns,
+                               (long)Cout, db, sign, accumulate);
+        return hip_ok();
+    }
     if (XS == XS_S1 && Cout == 1 && Gc == 1 && Goff == 0 && Cin % 32 == 0 && x0c % 4 == 0 && x1c % 4 == 0 &&
         Hin == Hout && Win == Wout) {                        // final_conv: VALU, one output row
         a.TH = 16; a.TW = 16;
@@ -742,8 +763,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.mask = sv.u; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = 1; d.Cin = C;
         d.accumulate = 0;
         CHECK(dgrad_vec(k, d, P.final_w));                                              // g_U (ReLU'd)
-        CHECK(wgrad<XS_UP>(k, ws.gU, C, 0, C, io.h, C, nullptr, 0, C, h, w, H, W, pg.up_w, 1.0f, 0, pg.up_b));
-        CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF));
+        // upsample conv wgrad as a stride-1 wgrad over the materialised up(h) (in dxpF, which
+        // the dgrad below overwrites); the gradient scale is shared with that dgrad
+        const float *gsu = grad_scale(k, ws.gU, HW * C);
+        hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
+        CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
+        CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
         CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
         hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
                            B, h, w, C, 1);

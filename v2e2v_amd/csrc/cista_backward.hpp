@@ -591,6 +591,116 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const WgradArgs a) {
     }
 }
 
+// --------------------------------------------------------------------------------------------
+// wgrad of the input-stage convs We (num_bins -> C/2) and Wi (1 -> C/2): CI <= 8 NCHW input
+// planes, Cout <= 32 output channels of G (channels [Goff, Goff + Cout) of a Gc-channel NHWC
+// tensor).  VALU: thread = (output channel tid & 31, pixel phase tid >> 5) accumulates CI x 9
+// taps; G tile (256 px x 32, stride 33) and the reflect-padded CI x 18 x 18 input halo in
+// LDS; blockIdx.x = split over 16 x 16 tiles; phases summed in a fixed order.
+// --------------------------------------------------------------------------------------------
+template <int CI>
+__global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradArgs a) {
+    __shared__ float Gt[256 * 33];
+    __shared__ float Xh[CI * 18 * 18];
+    const int tid = threadIdx.x, co = tid & 31, ph = tid >> 5;
+    float acc[CI][9];
+#pragma unroll
+    for (int c = 0; c < CI; ++c)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[c][t] = 0.0f;
+    float bsum = 0.0f;
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    for (int tile = blockIdx.x; tile < ntiles; tile += a.nsplit) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * 16, ox0 = tx * 16;
+        __syncthreads();
+        for (int i = tid; i < 256 * 32; i += 256) {
+            const int p = i >> 5, c = i & 31;
+            const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+            Gt[p * 33 + c] = (c < a.Cout && oy < a.Hout && ox < a.Wout)
+                                 ? a.G[(((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + c] : 0.0f;
+        }
+        for (int i = tid; i < CI * 324; i += 256) {
+            const int c = i / 324, hp = i - c * 324;
+            const int hy = hp / 18, hx = hp - hy * 18;
+            const int y = reflect_clamp(oy0 - 1 + hy, a.Hin), x = reflect_clamp(ox0 - 1 + hx, a.Win);
+            Xh[i] = a.X0[(((size_t)b * a.x0c + c) * a.Hin + y) * a.Win + x];
+        }
+        __syncthreads();
+        for (int p = ph; p < 256; p += 8) {
+            const float g = Gt[p * 33 + co];
+            bsum += g;
+            const int hb = (p >> 4) * 18 + (p & 15);
+#pragma unroll
+            for (int c = 0; c < CI; ++c)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[c][t] = fmaf(g, Xh[c * 324 + hb + (t / 3) * 18 + (t % 3)], acc[c][t]);
+        }
+    }
+    // sum the 8 phases in order 0..7 (phase 0 accumulates the others through LDS)
+    float *red = Gt;                                   // 32 x (CI*9 + 1) floats per round
+    constexpr int RS = CI * 9 + 1;
+    for (int src = 1; src < 8; ++src) {
+        __syncthreads();
+        if (ph == src) {
+#pragma unroll
+            for (int c = 0; c < CI; ++c)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) red[co * RS + c * 9 + t] = acc[c][t];
+            red[co * RS + CI * 9] = bsum;
+        }
+        __syncthreads();
+        if (ph == 0) {
+#pragma unroll
+            for (int c = 0; c < CI; ++c)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[c][t] += red[co * RS + c * 9 + t];
+            bsum += red[co * RS + CI * 9];
+        }
+    }
+    if (ph == 0 && co < a.Cout) {
+        float *part = a.partial + (size_t)blockIdx.x * a.Cout * CI * 9;
+#pragma unroll
+        for (int c = 0; c < CI; ++c)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) part[((size_t)co * CI + c) * 9 + t] = acc[c][t];
+        if (a.bpartial) a.bpartial[(size_t)blockIdx.x * a.Cout + co] = bsum;
+    }
+}
+
+// up = interpolate(x, 2x, bilinear, align_corners=False) materialised, NHWC (B,h,w,C) ->
+// (B,2h,2w,C), the operation order of the forward's STAGE_UP gather (base_layers.py:198), so
+// the upsample conv's wgrad can run as a stride-1 wgrad on it
+__global__ __launch_bounds__(256) void upsample2x_kernel(const float *x, float *up, int B, int h, int w, int C) {
+    const int c4 = C / 4, H = 2 * h, W = 2 * w;
+    const long total = (long)B * H * W * c4;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int q = (int)(idx % c4);
+    const long pix = idx / c4;
+    const int X = (int)(pix % W), Y = (int)((pix / W) % H), b = (int)(pix / ((long)W * H));
+    const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
+    const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
+    const int y0 = (int)sy, x0 = (int)sx;
+    const int y1 = y0 + (y0 < h - 1 ? 1 : 0), x1 = x0 + (x0 < w - 1 ? 1 : 0);
+    const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1, lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+    const float *base = x + (size_t)b * h * w * C + 4 * q;
+    const float4 v00 = *(const float4 *)(base + ((size_t)y0 * w + x0) * C);
+    const float4 v01 = *(const float4 *)(base + ((size_t)y0 * w + x1) * C);
+    const float4 v10 = *(const float4 *)(base + ((size_t)y1 * w + x0) * C);
+    const float4 v11 = *(const float4 *)(base + ((size_t)y1 * w + x1) * C);
+    float4 r;
+    r.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
+    r.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
+    r.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
+    r.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+    *(float4 *)(up + (size_t)pix * C + 4 * q) = r;
+}
+
 // dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9)
 __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *partial, int nsplit, long n,
                                                               float *dst, float sign, int accumulate) {
