@@ -35,6 +35,9 @@ sys.path.insert(0, ROOT)
 MACS_PER_FRAME_C64 = 22_793_011_200          # 180x240, C=64, depth 5, bins 5
 PEAK_F16_MFMA_TFLOPS = 2500.0                # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PASSES = 3
+PEAK_F32_MFMA_TFLOPS = 157.3                 # MI355X dense fp32 matrix (BASELINE.md framing)
+HBM_TBPS = 8.0                               # MI355X HBM3E
+BYTES_PER_FRAME = 34_387_200                 # 4*H*W*(num_bins + 2 + 3C): voxel, prev image, states in/out, frame
 
 
 def parse():
@@ -458,6 +461,15 @@ def main():
                        "precision": "split3-f16 MFMA (fp32 accumulate)"},
             "frames_per_s_per_gpu": round(value / world, 2),
             "tflops_effective": round(value * 2 * MACS_PER_FRAME_C64 / 1e12, 2),
+            # whole-path fractions of BASELINE.md's roofline framing, per GPU: algorithmic FLOPs
+            # and bytes per frame x frames/s over the peak
+            "path_fractions": {
+                "mfma_frac_vs_split3_peak": round(value / world * 2 * MACS_PER_FRAME_C64
+                                                  / (PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES * 1e12), 4),
+                "mfma_frac_vs_fp32_matrix_peak": round(value / world * 2 * MACS_PER_FRAME_C64
+                                                       / (PEAK_F32_MFMA_TFLOPS * 1e12), 4),
+                "hbm_frac": round(value / world * BYTES_PER_FRAME / (HBM_TBPS * 1e12), 5),
+                "hbm_gbps_algorithmic": round(value / world * BYTES_PER_FRAME / 1e9, 1)},
             "psnr_vs_ref": None if psnr_vs_ref is None else round(psnr_vs_ref, 2),
             "max_rel_err_vs_ref": rel_vs_ref,
             "outputs_finite": finite,

@@ -35,7 +35,7 @@ for step in "$@"; do
     vtests)
       # persistent-loop parity of every variant build (bit-exact batch vs single runs)
       for f in v2e2v_amd/variants/*.so; do
-        CISTA_HIP_LIB=$f timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -p no:cacheprovider -k "persistent or f3 or stage" > gpurun_out/vtests_$(basename $f .so).log 2>&1
+        CISTA_HIP_LIB=$f timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -p no:cacheprovider -k "stage or f3 or oracle_random or f1_sequence or batch" > gpurun_out/vtests_$(basename $f .so).log 2>&1
         rc=$?; echo "vtests $(basename $f) rc=$rc"; tail -1 gpurun_out/vtests_$(basename $f .so).log; ok $rc || exit $rc
       done ;;
     ab)

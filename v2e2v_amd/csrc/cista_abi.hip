@@ -183,7 +183,11 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if constexpr (HAS_SV)
         if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr) kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
+#if CISTA_XCD
+    dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
+#else
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
+#endif
     // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
     // the epilogue indexes outputs with 32-bit element offsets (pixel * Cout, x4 for out2)
     // and the double-buffered staging reads inputs with 32-bit element offsets
@@ -208,6 +212,9 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #ifndef CISTA_PF_MT
 #define CISTA_PF_MT 12
 #endif
+#ifndef CISTA_WIDE
+#define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
+#endif
 template <int STAGE, int EPI, int G>
 int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
@@ -220,6 +227,9 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         return CISTA_ERR_UNSUPPORTED;
     } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2)) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
+        constexpr bool FWD = STAGE == STAGE_S1;
+        if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
+            if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
         if constexpr (G == 4) {
             if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
         } else {
