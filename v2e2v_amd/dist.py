@@ -3,7 +3,8 @@
 Inference has no exchange step -- sequences are independent (no BN/IN), so each
 rank reconstructs its own shard and nothing crosses xGMI on the data path.  The only
 collectives are the benchmark's barrier and max-over-ranks timing (RCCL, or gloo on CPU for the
-tests).  DDP for BPTT training (one gradient all-reduce per step) arrives with the backward.
+tests).  BPTT training wraps the module in DistributedDataParallel (one bucketed RCCL gradient
+all-reduce per step, bench.py --mode train).
 """
 from __future__ import annotations
 
