@@ -501,7 +501,10 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
     return s;
 }
 
-constexpr int WG_BLOCKS = 1024;          // wgrad workgroups per launch (splits x cout/cin blocks)
+#ifndef CISTA_WG_BLOCKS
+#define CISTA_WG_BLOCKS 1024
+#endif
+constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
