@@ -399,15 +399,17 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
     //                group cg = tid >> 6 (halo columns 8 cg .. 8 cg + 9)
     const int cq = tid & 15, pg = tid >> 4;
     const int xq = tid & 7, xr = (tid >> 3) & 7, xcg = (tid >> 6) & 1;
-    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
+    // the global loads of BOTH operands of the next pixel tile are issued right after this
+    // tile's LDS image is written, so they land under its MFMAs (register double buffer);
+    // the split + LDS stores of a tile wait only for loads issued a whole tile earlier
+    float4 gv[8], xv[10];
+    auto load_tile = [&](int tile) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
         tt /= a.tiles_x;
         const int ty = tt % a.tiles_y;
         const int b = tt / a.tiles_y;
         const int oy0 = ty * WS_TH, ox0 = tx * WS_TW;
-        // global loads of both operands first (latency overlap), then split + LDS stores
-        float4 gv[8], xv[10];
         if (tid < 192) {
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
@@ -424,6 +426,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
             for (int j = 0; j < 10; ++j)
                 xv[j] = wg_load_x4<XS_S1>(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 4 * xq);
         }
+    };
+    if ((int)blockIdx.y < ntiles) load_tile(blockIdx.y);
+    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
         __syncthreads();                       // the previous tile's fragment reads are done
         if (tid < 192) {
             if (do_bias) {
@@ -471,6 +476,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
             }
         }
         __syncthreads();
+        if (tile + a.nsplit < ntiles) load_tile(tile + a.nsplit);
         const int kg = lane >> 4, r16 = lane & 15;
 #pragma unroll
         for (int s = 0; s < WS_NPX / 32; ++s) {
