@@ -143,3 +143,28 @@ def test_v2e_oracle_properties():
     assert n > 0 and vox.min() >= 0 and vox.max() > 0            # brightening: ON events only
     vox, _ = vo.V2EOracle(**det).forward(ramp[:, ::-1].copy(), np.linspace(0, 0.04, 5)[None])
     assert vox.max() <= 0 and vox.min() < 0
+
+
+@pytest.mark.parametrize("tag", ["default", "stress"])
+def test_torch_cpu_restatement_f1(golden, tag):
+    """The PyTorch-CPU restatement (bench.py's cpu_baseline leg) against the same vectors."""
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU
+    d = golden("f1_64x64.npz")
+    params = default_params() if tag == "default" else fx.stress_params(64, 5, 5)
+    recs, st = CistaLSTCTorchCPU(params, 5).run_sequence(d["voxels"])
+    for f in range(3):
+        assert rel_err(recs[f], d[f"{tag}_rec{f}"]) < TOL32
+    for k, v in zip(["c_lstc", "z", "h", "c"], [st[0], st[1], st[2][0], st[2][1]]):
+        assert rel_err(v, d[f"{tag}_state_{k}"]) < TOLST, k
+    recs64, _ = CistaLSTCTorchCPU(params, 5, torch.float64).run_sequence(d["voxels"])
+    for f in range(3):
+        assert np.abs(recs64[f] - d[f"{tag}_rec{f}_f64"]).max() < TOL64
+
+
+def test_torch_cpu_restatement_f2(golden):
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU
+    d = golden("f2_32x48_c32_d2.npz")
+    recs, st = CistaLSTCTorchCPU(fx.stress_params(32, 2, 5, seed=11), 2).run_sequence(d["voxels"])
+    for f in range(4):
+        assert rel_err(recs[f], d[f"rec{f}"]) < TOL32
+    assert rel_err(st[1], d["state_z"]) < TOLST
