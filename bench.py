@@ -326,6 +326,14 @@ def time_layers(torch, model, lib_mod, vox, B, H, W, device, reps):
             res[name] = dict(ms=ms, macs=macs, launches_per_frame=per_frame,
                              tflops=2 * macs / (ms * 1e-3) / 1e12)
         torch.cuda.synchronize()
+    # the input stage computes W0 too (one composed linear map, input_w0_kernel): the W0 layer
+    # launches nothing, so its work is credited to the fused launch
+    if "W0" in res and res["W0"]["ms"] < 0.05 * res["input"]["ms"]:
+        w0 = res.pop("W0")
+        res["input+W0"] = dict(res.pop("input"))
+        r = res["input+W0"]
+        r["macs"] += w0["macs"]
+        r["tflops"] = 2 * r["macs"] / (r["ms"] * 1e-3) / 1e12
     return res
 
 

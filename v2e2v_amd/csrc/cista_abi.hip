@@ -40,7 +40,7 @@ ConvShape conv_shape(int id, int C) {
 struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
-    size_t wE, wI, bIn, wF, bF, lambda;
+    size_t wE, wI, bIn, wF, bF, lambda, wC, bC;
     size_t total;
 };
 
@@ -70,6 +70,8 @@ Layout make_layout(const cista_config &cfg) {
     L.wF = off; off = align_up(off + (size_t)9 * C * 4);
     L.bF = off; off = align_up(off + 4);
     L.lambda = off; off = align_up(off + (size_t)2 * C * 4);
+    L.wC = off; off = align_up(off + (size_t)9 * 25 * (nb + 1) * C * 4);   // fused input + W0
+    L.bC = off; off = align_up(off + (size_t)C * 4);
     L.total = off;
     return L;
 }
@@ -212,12 +214,22 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #ifndef CISTA_PF_MT
 #define CISTA_PF_MT 12
 #endif
+#ifndef CISTA_S2DB
+#define CISTA_S2DB 0      // stride-2 W0: 0 single-buffered 128-px tiles; 1/2 double-buffered 64-px
+#endif
 #ifndef CISTA_WIDE
 #define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
 #endif
 template <int STAGE, int EPI, int G>
 int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
+#if CISTA_S2DB == 1
+        // double-buffered K loop: 64-pixel tiles keep two stride-2 halo images (17x17 px)
+        // within the 80 KiB LDS of two workgroups per CU
+        if (a.N % 64 == 0) return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 5>(a, st);
+#elif CISTA_S2DB == 2
+        if (a.N % 64 == 0) return launch_conv_cfg<1, 4, 4, 1, STAGE, EPI, G, true, 5>(a, st);
+#endif
         if (a.N % 64 == 0) return launch_conv_cfg<2, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N % 32 == 0) return launch_conv_cfg<2, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
@@ -307,8 +319,15 @@ struct Frame {
     float *y;              // relu(Dg.conv(z))                            (B,h,w,C)
     float *lg;             // ConvLSTM gates (i, r, o, g) post-activation (B,h,w,4C)
     float *u;              // relu(upsamp_conv(...))                      (B,H,W,C)
+    bool need_full;        // the input stage must write x_full (the backward's recompute)
     hipStream_t st;
 };
+
+// input stage and W0 as one composed linear map (input_w0_kernel) for 1..8 bins
+#ifndef CISTA_FUSED_IN
+#define CISTA_FUSED_IN 1
+#endif
+inline bool fused_input(const cista_config &cfg) { return CISTA_FUSED_IN && cfg.num_bins <= 8; }
 
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
@@ -320,6 +339,25 @@ int run_layer(const Frame &f, int layer, int it = 0) {
     ConvArgs a;
     switch (layer) {
         case CISTA_LAYER_INPUT: {                                      // e2v_model.py:62-64
+            if (fused_input(*f.cfg) && !f.need_full) {                 // ... and W0, :66
+                FusedInArgs fa;
+                fa.events = f.events; fa.prev = f.prev_image;
+                fa.E = blob<float>(f.packed, f.L.wC); fa.bias = blob<float>(f.packed, f.L.bC);
+                fa.out = f.x1; fa.B = B; fa.H = f.H; fa.W = f.W; fa.h = h; fa.w = w; fa.C = C;
+                const long most = (long)B * (h > 2 ? h - 2 : 1) * (w > 2 ? w - 2 : 1);
+                const dim3 g2((unsigned)((most + 255) / 256), 9);
+                const size_t lds = (size_t)256 * (C + 1) * 4;
+                switch (f.cfg->num_bins) {
+#define NBCASE(n)                                                                           \
+    case n:                                                                                 \
+        if (!allow_big_lds((const void *)input_w0_kernel<n>)) return CISTA_ERR_HIP;        \
+        hipLaunchKernelGGL(input_w0_kernel<n>, g2, dim3(256), lds, f.st, fa);              \
+        break;
+                    NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7) NBCASE(8)
+#undef NBCASE
+                }
+                return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+            }
             InputArgs ia;
             ia.events = f.events; ia.prev = f.prev_image;
             ia.wE = blob<float>(f.packed, f.L.wE); ia.wI = blob<float>(f.packed, f.L.wI);
@@ -345,6 +383,7 @@ int run_layer(const Frame &f, int layer, int it = 0) {
             return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
         }
         case CISTA_LAYER_W0:                                           // e2v_model.py:66
+            if (fused_input(*f.cfg) && !f.need_full) return CISTA_OK;  // done by the input stage
             a = conv_args(f.packed, f.L, CV_W0, C, B, f.H, f.W, h, w, f.full, C, nullptr, 0);
             a.out0 = f.x1;
             return launch_conv<STAGE_S2, EPI_BIAS, 1>(a, f.st);
@@ -876,6 +915,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         memset(&f, 0, sizeof(f));
         f.cfg = k.cfg; f.packed = k.packed; f.L = k.L; f.B = B; f.H = H; f.W = W; f.h = h; f.w = w;
         f.C = C; f.events = io.events; f.prev_image = io.prev_image; f.full = xfull; f.st = st;
+        f.need_full = true;
         CHECK(run_layer(f, CISTA_LAYER_INPUT));
     }
     CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
@@ -969,6 +1009,12 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
                        p->Wi_w, blobw<float>(packed, L.wI), half, 1);
     hipLaunchKernelGGL(final_weight_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st,
                        p->final_w, blobw<float>(packed, L.wF), C);
+    {
+        const long ne = 9L * 25 * (nb + 1) * C + C;
+        hipLaunchKernelGGL(compose_in_w0_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+                           p->We_w, p->Wi_w, p->We_b, p->Wi_b, p->W0_w, p->W0_b,
+                           blobw<float>(packed, L.wC), blobw<float>(packed, L.bC), nb, C);
+    }
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     char *pb = static_cast<char *>(packed);
     if (hipMemcpyAsync(pb + L.bIn, p->We_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||

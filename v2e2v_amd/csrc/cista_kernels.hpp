@@ -425,7 +425,8 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
     };
     if constexpr (NI > 0) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
-        static_assert(STAGE == STAGE_S1 || STAGE == STAGE_ZP2, "double-buffered staging: stride-1 inputs");
+        static_assert(STAGE == STAGE_S1 || STAGE == STAGE_S2 || STAGE == STAGE_ZP2,
+                      "double-buffered staging: direct (reflect / zero padded) inputs");
         int spix[NI], shp[NI], sg[NI];
         stage_pixels<STAGE, NI>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
         {
@@ -950,6 +951,130 @@ __global__ __launch_bounds__(256) void input_stage_kernel_nb(const InputArgs a) 
         const int p = e / C, c = e - p * C;
         const float *srow = tile + p * ld + c;
         dst[i] = make_float4(srow[0], srow[1], srow[2], srow[3]);
+    }
+}
+
+// ------------------------------------------------------------------------------------------
+// Fused input stage + W0 (e2v_model.py:62-66).  There is no activation between We/Wi and W0,
+// so x1 = W0(cat(We(ev), Wi(img))) is ONE linear map of the (nb+1)-channel input: a 5x5
+// stride-2 window around (2oy, 2ox) with composed weights E = W0 (x) cat(We, Wi).  The two
+// reflect paddings fold into the weights: an output row is top (oy = 0), interior or bottom
+// (oy = h-1), likewise for columns, and each of the 3 x 3 classes has its own composed E
+// (composed in fp64 at pack time).  x_full (11 MB per sample, written then re-read) and
+// 4 x of the MACs disappear.  Needs even H, W >= 4 (the ABI enforces it).
+// ------------------------------------------------------------------------------------------
+// offset (relative to 2o) of the input row read by W0 tap k then the inner conv's tap d
+__device__ __forceinline__ int fused_in_offset(int cls, int k, int d) {
+    if (cls == 1) return k + d - 2;
+    const int n = 8;                                // any even size >= 4: the offsets do not depend on it
+    const int o = cls == 0 ? 0 : n / 2 - 1;
+    return reflect_clamp(reflect_clamp(2 * o + k - 1, n) + d - 1, n) - 2 * o;
+}
+
+// E[cls][off 25][cin nb+1][cout C] (fp32) and the composed bias bC[C]
+__global__ void compose_in_w0_kernel(const float *We, const float *Wi, const float *bE, const float *bI,
+                                     const float *W0, const float *b0, float *E, float *bC, int nb, int C) {
+    const int K = nb + 1, half = C / 2;
+    const long total = 9L * 25 * K * C;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total + C) return;
+    if (idx >= total) {                             // bias: b0 + sum_{m,tap} W0 * b_full[m]
+        const int co = (int)(idx - total);
+        double acc = b0[co];
+        for (int m = 0; m < C; ++m) {
+            const double bm = m < half ? bE[m] : bI[m - half];
+            for (int t = 0; t < 9; ++t) acc += (double)W0[((size_t)co * C + m) * 9 + t] * bm;
+        }
+        bC[co] = (float)acc;
+        return;
+    }
+    const int co = (int)(idx % C);
+    const int ci = (int)((idx / C) % K);
+    const int off = (int)((idx / ((long)C * K)) % 25);
+    const int cls = (int)(idx / ((long)C * K * 25));
+    const int rc = cls / 3, cc = cls % 3, oy = off / 5 - 2, ox = off % 5 - 2;
+    double acc = 0.0;
+    for (int ky = 0; ky < 3; ++ky)
+        for (int dy = 0; dy < 3; ++dy) {
+            if (fused_in_offset(rc, ky, dy) != oy) continue;
+            for (int kx = 0; kx < 3; ++kx)
+                for (int dx = 0; dx < 3; ++dx) {
+                    if (fused_in_offset(cc, kx, dx) != ox) continue;
+                    const int t0 = ky * 3 + kx, t1 = dy * 3 + dx;
+                    if (ci < nb) {
+                        for (int m = 0; m < half; ++m)
+                            acc += (double)W0[((size_t)co * C + m) * 9 + t0] *
+                                   (double)We[((size_t)m * nb + ci) * 9 + t1];
+                    } else {
+                        for (int m = 0; m < half; ++m)
+                            acc += (double)W0[((size_t)co * C + half + m) * 9 + t0] * (double)Wi[(size_t)m * 9 + t1];
+                    }
+                }
+        }
+    E[idx] = (float)acc;
+}
+
+struct FusedInArgs {
+    const float *events;   // (B, nb, H, W)
+    const float *prev;     // (B, 1, H, W)
+    const float *E;        // [9][25 * (nb+1)][C]
+    const float *bias;     // [C]
+    float *out;            // x1 (B, h, w, C)
+    int B, H, W, h, w, C;
+};
+
+// grid (ceil(B * pixels of the largest class / 256), 9): blockIdx.y = class (uniform, so the
+// composed weights are wave-uniform scalar loads); thread = one output pixel of that class.
+// (Two pixels per thread sharing each weight load measured 2.4x slower: 0.91 vs 0.38 ms.)
+template <int NB>
+__global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
+    extern __shared__ float tile[];                 // [256][C + 1]
+    constexpr int K = 25 * (NB + 1);                // composed taps per class
+    const int cls = blockIdx.y, rc = cls / 3, cc = cls % 3;
+    const int r0 = rc == 0 ? 0 : rc == 1 ? 1 : a.h - 1, nr = rc == 1 ? a.h - 2 : 1;
+    const int c0 = cc == 0 ? 0 : cc == 1 ? 1 : a.w - 1, nc = cc == 1 ? a.w - 2 : 1;
+    const long total = (long)a.B * nr * nc;
+    const long p0 = (long)blockIdx.x * 256;
+    if (p0 >= total) return;                        // whole block: before any barrier
+    const long pc = p0 + threadIdx.x < total ? p0 + threadIdx.x : total - 1;
+    const int oy = r0 + (int)((pc / nc) % nr), ox = c0 + (int)(pc % nc);
+    const int b = (int)(pc / ((long)nr * nc));
+    const size_t plane = (size_t)a.H * a.W;
+    const float *ev = a.events + (size_t)b * NB * plane, *im = a.prev + (size_t)b * plane;
+    const int C = a.C, ld = C + 1;
+    const float *E = a.E + (size_t)cls * K * C;
+    float *row = tile + threadIdx.x * ld;
+    // 32 output channels per pass; the window's inputs are re-read per pass (L1-resident)
+    for (int q0 = 0; q0 < C; q0 += 32) {
+        float acc[32];
+#pragma unroll
+        for (int i = 0; i < 32; ++i) acc[i] = a.bias[q0 + i];
+        for (int t = 0; t < 25; ++t) {
+            // out-of-image window positions carry zero weight; the clamp keeps the load in bounds
+            const int y = min(max(2 * oy + t / 5 - 2, 0), a.H - 1), x = min(max(2 * ox + t % 5 - 2, 0), a.W - 1);
+            const size_t o = (size_t)y * a.W + x;
+            float v[NB + 1];
+#pragma unroll
+            for (int ci = 0; ci < NB; ++ci) v[ci] = ev[(size_t)ci * plane + o];
+            v[NB] = im[o];
+            const float *wt = E + (size_t)t * (NB + 1) * C + q0;
+#pragma unroll
+            for (int ci = 0; ci <= NB; ++ci)
+#pragma unroll
+                for (int i = 0; i < 32; ++i) acc[i] = fmaf(v[ci], wt[(size_t)ci * C + i], acc[i]);
+        }
+#pragma unroll
+        for (int i = 0; i < 32; ++i) row[q0 + i] = acc[i];
+    }
+    __syncthreads();
+    const int nvalid = (int)((total - p0) < 256 ? (total - p0) : 256);
+    const int q4 = C / 4;
+    for (int i = threadIdx.x; i < nvalid * q4; i += 256) {
+        const int p = i / q4, c = (i - p * q4) * 4;
+        const long pp = p0 + p;
+        const int y = r0 + (int)((pp / nc) % nr), x = c0 + (int)(pp % nc), bb = (int)(pp / ((long)nr * nc));
+        const float *srow = tile + p * ld + c;
+        *(float4 *)(a.out + (((size_t)bb * a.h + y) * a.w + x) * C + c) = make_float4(srow[0], srow[1], srow[2], srow[3]);
     }
 }
 
