@@ -188,6 +188,20 @@ def test_oracle_random(C, depth, B, H, W):
     assert rel_err(st[2][1], o_st[2][1]) < TOL
 
 
+@pytest.mark.parametrize("nb,H,W", [(1, 10, 12), (3, 20, 14), (8, 8, 18), (9, 12, 10)])
+def test_num_bins(nb, H, W):
+    """Bin counts other than 5: the fused input stage + W0 (input_w0_kernel<NB>, 1..8 bins) and
+    the unfused fallback (> 8 bins) against the oracle, with border rows/columns on every side."""
+    params = fx.stress_params(32, 2, nb, seed=200 + nb)
+    vox = fx.synthetic_voxels(2, 2, nb, H, W, n_events=max(8, fx.density_matched_events(H, W)),
+                              seed=nb * 31 + H)
+    m = make_model(C=32, depth=2, nb=nb, params=params)
+    recs, st = run_seq(m, vox)
+    o_recs, o_st = CistaLSTCOracle(params, 2).run_sequence(vox)
+    assert rel_err(recs, o_recs) < TOL
+    assert rel_err(st[1], o_st[1]) < TOL
+
+
 def test_partial_none_states():
     """prev_states entries are None-able independently (reference e2v_model.py:68,82)."""
     params = fx.stress_params(64, 2, 5, seed=5)
