@@ -19,7 +19,7 @@ inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
 // ---------------------------------------------------------------------------------------
 // packed parameter blob layout
 // ---------------------------------------------------------------------------------------
-enum ConvId { CV_W0, CV_P0, CV_GATES, CV_OUTG, CV_D, CV_P, CV_DG, CV_LSTM, CV_UP, CV_COUNT };
+enum ConvId { CV_W0, CV_P0, CV_GATES, CV_OUTG, CV_D, CV_P, CV_DG, CV_LSTM, CV_UP, CV_IN, CV_COUNT };
 
 struct ConvShape { int cout, cin, G; };
 
@@ -33,6 +33,7 @@ ConvShape conv_shape(int id, int C) {
         case CV_P: return {2 * C, C, 1};
         case CV_DG: return {C, 2 * C, 1};
         case CV_LSTM: return {4 * C, 2 * C, 4};      // (in, remember, out, cell) base_layers.py:116
+        case CV_IN: return {C, 32, 1};               // composed input stage + W0 over the s2d input
         default: return {C, C, 1};                   // CV_UP
     }
 }
@@ -40,7 +41,7 @@ ConvShape conv_shape(int id, int C) {
 struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
-    size_t wE, wI, bIn, wF, bF, lambda, wC, bC;
+    size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS;
     size_t total;
 };
 
@@ -72,6 +73,8 @@ Layout make_layout(const cista_config &cfg) {
     L.lambda = off; off = align_up(off + (size_t)2 * C * 4);
     L.wC = off; off = align_up(off + (size_t)9 * 25 * (nb + 1) * C * 4);   // fused input + W0
     L.bC = off; off = align_up(off + (size_t)C * 4);
+    L.wS = off; off = align_up(off + (size_t)C * 32 * 9 * 4);            // CV_IN, reference layout
+    L.bS = off; off = align_up(off + (size_t)C * 4);
     L.total = off;
     return L;
 }
@@ -328,6 +331,11 @@ struct Frame {
 #define CISTA_FUSED_IN 1
 #endif
 inline bool fused_input(const cista_config &cfg) { return CISTA_FUSED_IN && cfg.num_bins <= 8; }
+#ifndef CISTA_S2D_IN
+#define CISTA_S2D_IN 1
+#endif
+// ... with its interior on MFMA (space-to-depth input, 4 (nb+1) <= 32 channels)
+inline bool s2d_input(const cista_config &cfg) { return CISTA_S2D_IN && cfg.num_bins <= 7; }
 
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
@@ -344,8 +352,21 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 fa.events = f.events; fa.prev = f.prev_image;
                 fa.E = blob<float>(f.packed, f.L.wC); fa.bias = blob<float>(f.packed, f.L.bC);
                 fa.out = f.x1; fa.B = B; fa.H = f.H; fa.W = f.W; fa.h = h; fa.w = w; fa.C = C;
-                const long most = (long)B * (h > 2 ? h - 2 : 1) * (w > 2 ? w - 2 : 1);
-                const dim3 g2((unsigned)((most + 255) / 256), 9);
+                fa.border_only = 0;
+                long most = (long)B * (h > 2 ? h - 2 : 1) * (w > 2 ? w - 2 : 1);
+                if (s2d_input(*f.cfg)) {
+                    // interior on MFMA: s2d input (in x_full's space) -> 3x3 split-f16 conv; the
+                    // conv's reflect-padded border outputs are then overwritten by the VALU pass
+                    const long ns = (long)B * h * w * 32;
+                    hipLaunchKernelGGL(s2d_input_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, f.st,
+                                       f.events, f.prev_image, f.full, B, f.cfg->num_bins, f.H, f.W);
+                    a = conv_args(f.packed, f.L, CV_IN, C, B, h, w, h, w, f.full, 32, nullptr, 0);
+                    a.out0 = f.x1;
+                    if (const int sc = launch_conv<STAGE_S1, EPI_BIAS, 1>(a, f.st)) return sc;
+                    fa.border_only = 1;
+                    most = (long)B * (h > w ? h : w);
+                }
+                const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9);
                 const size_t lds = (size_t)256 * (C + 1) * 4;
                 switch (f.cfg->num_bins) {
 #define NBCASE(n)                                                                           \
@@ -977,10 +998,20 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int C = cfg->base_channels, nb = cfg->num_bins;
     const Layout L = make_layout(*cfg);
+    {
+        const long ne = 9L * 25 * (nb + 1) * C + C;
+        hipLaunchKernelGGL(compose_in_w0_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
+                           p->We_w, p->Wi_w, p->We_b, p->Wi_b, p->W0_w, p->W0_b,
+                           blobw<float>(packed, L.wC), blobw<float>(packed, L.bC), nb, C);
+        const int ns = C * 32 * 9 + C;
+        hipLaunchKernelGGL(s2d_weight_kernel, dim3((ns + 255) / 256), dim3(256), 0, st,
+                           (const float *)blobw<float>(packed, L.wC), (const float *)blobw<float>(packed, L.bC),
+                           blobw<float>(packed, L.wS), blobw<float>(packed, L.bS), nb, C);
+    }
     const float *ws[CV_COUNT] = {p->W0_w, p->P0_w, p->gates_w, p->out_gates_w, p->D_w, p->P_w,
-                                 p->Dg_w, p->lstm_w, p->up_w};
+                                 p->Dg_w, p->lstm_w, p->up_w, blobw<float>(packed, L.wS)};
     const float *bs[CV_COUNT] = {p->W0_b, p->P0_b, p->gates_b, p->out_gates_b, p->D_b, p->P_b,
-                                 p->Dg_b, p->lstm_b, p->up_b};
+                                 p->Dg_b, p->lstm_b, p->up_b, blobw<float>(packed, L.bS)};
     for (int i = 0; i < CV_COUNT; ++i) {
         const ConvShape s = conv_shape(i, C);
         PackArgs a;
@@ -1009,12 +1040,6 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
                        p->Wi_w, blobw<float>(packed, L.wI), half, 1);
     hipLaunchKernelGGL(final_weight_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st,
                        p->final_w, blobw<float>(packed, L.wF), C);
-    {
-        const long ne = 9L * 25 * (nb + 1) * C + C;
-        hipLaunchKernelGGL(compose_in_w0_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,
-                           p->We_w, p->Wi_w, p->We_b, p->Wi_b, p->W0_w, p->W0_b,
-                           blobw<float>(packed, L.wC), blobw<float>(packed, L.bC), nb, C);
-    }
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     char *pb = static_cast<char *>(packed);
     if (hipMemcpyAsync(pb + L.bIn, p->We_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||

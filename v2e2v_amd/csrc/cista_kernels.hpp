@@ -1021,6 +1021,7 @@ struct FusedInArgs {
     const float *bias;     // [C]
     float *out;            // x1 (B, h, w, C)
     int B, H, W, h, w, C;
+    int border_only;       // 1: grid.y = 8 border classes (the interior came from the MFMA conv)
 };
 
 // grid (ceil(B * pixels of the largest class / 256), 9): blockIdx.y = class (uniform, so the
@@ -1030,7 +1031,7 @@ template <int NB>
 __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
     extern __shared__ float tile[];                 // [256][C + 1]
     constexpr int K = 25 * (NB + 1);                // composed taps per class
-    const int cls = blockIdx.y, rc = cls / 3, cc = cls % 3;
+    const int cls = a.border_only && blockIdx.y >= 4 ? blockIdx.y + 1 : blockIdx.y, rc = cls / 3, cc = cls % 3;
     const int r0 = rc == 0 ? 0 : rc == 1 ? 1 : a.h - 1, nr = rc == 1 ? a.h - 2 : 1;
     const int c0 = cc == 0 ? 0 : cc == 1 ? 1 : a.w - 1, nc = cc == 1 ? a.w - 2 : 1;
     const long total = (long)a.B * nr * nc;
@@ -1076,6 +1077,47 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
         const float *srow = tile + p * ld + c;
         *(float4 *)(a.out + (((size_t)bb * a.h + y) * a.w + x) * C + c) = make_float4(srow[0], srow[1], srow[2], srow[3]);
     }
+}
+
+// Interior pixels on MFMA: a 2x2 space-to-depth of the (nb+1)-channel input turns the 5x5
+// stride-2 window into a 3x3 stride-1 window over 4(nb+1) <= 32 channels at half resolution,
+// i.e. an ordinary conv3x3_split3 launch.  s2d channel s = (py*2 + px)*(nb+1) + ci.
+__global__ void s2d_input_kernel(const float *events, const float *prev, float *out, int B, int nb,
+                                 int H, int W) {
+    const int h = H / 2, w = W / 2, K = nb + 1;
+    const long total = (long)B * h * w * 32;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int s = (int)(idx & 31);
+    const long pix = idx >> 5;
+    const int X = (int)(pix % w), Y = (int)((pix / w) % h), b = (int)(pix / ((long)w * h));
+    float v = 0.f;
+    if (s < 4 * K) {
+        const int ph = s / K, ci = s - ph * K, y = 2 * Y + (ph >> 1), x = 2 * X + (ph & 1);
+        const size_t plane = (size_t)H * W, o = (size_t)y * W + x;
+        v = ci < nb ? events[((size_t)b * nb + ci) * plane + o] : prev[(size_t)b * plane + o];
+    }
+    out[idx] = v;
+}
+
+// reference-layout (C, 32, 3, 3) weights of that conv from the interior class of E, + bias
+__global__ void s2d_weight_kernel(const float *E, const float *bC, float *Ws, float *bS, int nb, int C) {
+    const int K = nb + 1;
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= C * 32 * 9 + C) return;
+    if (idx >= C * 32 * 9) {
+        bS[idx - C * 32 * 9] = bC[idx - C * 32 * 9];
+        return;
+    }
+    const int tap = idx % 9, s = (idx / 9) % 32, co = idx / (9 * 32);
+    float v = 0.f;
+    if (s < 4 * K) {
+        const int ph = s / K, ci = s - ph * K;
+        const int offy = 2 * (tap / 3 - 1) + (ph >> 1), offx = 2 * (tap % 3 - 1) + (ph & 1);
+        if (offy <= 2 && offx <= 2)
+            v = E[((size_t)(4 * 25 + (offy + 2) * 5 + (offx + 2)) * K + ci) * C + co];
+    }
+    Ws[idx] = v;
 }
 
 // ------------------------------------------------------------------------------------------
