@@ -357,16 +357,24 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 if (s2d_input(*f.cfg)) {
                     // interior on MFMA: s2d input (in x_full's space) -> 3x3 split-f16 conv; the
                     // conv's reflect-padded border outputs are then overwritten by the VALU pass
-                    const long ns = (long)B * h * w * 32;
-                    hipLaunchKernelGGL(s2d_input_kernel, dim3((unsigned)((ns + 255) / 256)), dim3(256), 0, f.st,
-                                       f.events, f.prev_image, f.full, B, f.cfg->num_bins, f.H, f.W);
+                    const dim3 gs((unsigned)(((long)B * h * w + 255) / 256));
+                    switch (f.cfg->num_bins) {
+#define NBCASE(n)                                                                                  \
+    case n:                                                                                        \
+        hipLaunchKernelGGL(s2d_input_kernel<n>, gs, dim3(256), 0, f.st, f.events, f.prev_image,   \
+                           f.full, B, f.H, f.W);                                                  \
+        break;
+                        NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7)
+#undef NBCASE
+                    }
                     a = conv_args(f.packed, f.L, CV_IN, C, B, h, w, h, w, f.full, 32, nullptr, 0);
                     a.out0 = f.x1;
                     if (const int sc = launch_conv<STAGE_S1, EPI_BIAS, 1>(a, f.st)) return sc;
                     fa.border_only = 1;
                     most = (long)B * (h > w ? h : w);
                 }
-                const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9);
+                const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9,
+                              fa.border_only ? C / 32 : 1);
                 const size_t lds = (size_t)256 * (C + 1) * 4;
                 switch (f.cfg->num_bins) {
 #define NBCASE(n)                                                                           \

@@ -1045,8 +1045,10 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
     const int C = a.C, ld = C + 1;
     const float *E = a.E + (size_t)cls * K * C;
     float *row = tile + threadIdx.x * ld;
-    // 32 output channels per pass; the window's inputs are re-read per pass (L1-resident)
-    for (int q0 = 0; q0 < C; q0 += 32) {
+    // 32 output channels per pass; the window's inputs are re-read per pass (L1-resident);
+    // gridDim.z splits the channels over workgroups (the border pass has few pixels)
+    const int qn = C / gridDim.z, qbeg = blockIdx.z * qn;
+    for (int q0 = qbeg; q0 < qbeg + qn; q0 += 32) {
         float acc[32];
 #pragma unroll
         for (int i = 0; i < 32; ++i) acc[i] = a.bias[q0 + i];
@@ -1069,9 +1071,9 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
     }
     __syncthreads();
     const int nvalid = (int)((total - p0) < 256 ? (total - p0) : 256);
-    const int q4 = C / 4;
+    const int q4 = qn / 4;
     for (int i = threadIdx.x; i < nvalid * q4; i += 256) {
-        const int p = i / q4, c = (i - p * q4) * 4;
+        const int p = i / q4, c = qbeg + (i - p * q4) * 4;
         const long pp = p0 + p;
         const int y = r0 + (int)((pp / nc) % nr), x = c0 + (int)(pp % nc), bb = (int)(pp / ((long)nr * nc));
         const float *srow = tile + p * ld + c;
@@ -1082,22 +1084,34 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
 // Interior pixels on MFMA: a 2x2 space-to-depth of the (nb+1)-channel input turns the 5x5
 // stride-2 window into a 3x3 stride-1 window over 4(nb+1) <= 32 channels at half resolution,
 // i.e. an ordinary conv3x3_split3 launch.  s2d channel s = (py*2 + px)*(nb+1) + ci.
-__global__ void s2d_input_kernel(const float *events, const float *prev, float *out, int B, int nb,
-                                 int H, int W) {
-    const int h = H / 2, w = W / 2, K = nb + 1;
-    const long total = (long)B * h * w * 32;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
-    const int s = (int)(idx & 31);
-    const long pix = idx >> 5;
+// thread = one half-resolution pixel: float2 loads of its 2x2 block per plane (coalesced
+// across the row), one 128-byte run of 32 channels out.
+template <int NB>
+__global__ __launch_bounds__(256) void s2d_input_kernel(const float *events, const float *prev, float *out,
+                                                        int B, int H, int W) {
+    constexpr int K = NB + 1;
+    static_assert(4 * K <= 32, "space-to-depth channels");
+    const int h = H / 2, w = W / 2;
+    const long pix = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (pix >= (long)B * h * w) return;
     const int X = (int)(pix % w), Y = (int)((pix / w) % h), b = (int)(pix / ((long)w * h));
-    float v = 0.f;
-    if (s < 4 * K) {
-        const int ph = s / K, ci = s - ph * K, y = 2 * Y + (ph >> 1), x = 2 * X + (ph & 1);
-        const size_t plane = (size_t)H * W, o = (size_t)y * W + x;
-        v = ci < nb ? events[((size_t)b * nb + ci) * plane + o] : prev[(size_t)b * plane + o];
+    const size_t plane = (size_t)H * W;
+    float v[32];
+#pragma unroll
+    for (int i = 4 * K; i < 32; ++i) v[i] = 0.f;
+#pragma unroll
+    for (int ci = 0; ci < K; ++ci) {
+        const float *src = ci < NB ? events + ((size_t)b * NB + ci) * plane : prev + (size_t)b * plane;
+#pragma unroll
+        for (int py = 0; py < 2; ++py) {
+            const float2 q = *(const float2 *)(src + (size_t)(2 * Y + py) * W + 2 * X);
+            v[(py * 2) * K + ci] = q.x;
+            v[(py * 2 + 1) * K + ci] = q.y;
+        }
     }
-    out[idx] = v;
+    float4 *o = (float4 *)(out + pix * 32);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = make_float4(v[4 * i], v[4 * i + 1], v[4 * i + 2], v[4 * i + 3]);
 }
 
 // reference-layout (C, 32, 3, 3) weights of that conv from the interior class of E, + bias
