@@ -23,9 +23,16 @@ def layer_of(name):
     m = re.search(r"conv3x3_split3<([^>]*)>", name)
     if m:
         args = [x.strip() for x in m.group(1).split(",")]
-        return CONV_LAYER.get((int(args[4]), int(args[5]))), "conv3x3_split3<" + ",".join(args) + ">"
+        kn = "conv3x3_split3<" + ",".join(args) + ">"
+        if (int(args[4]), int(args[5])) == (0, 0) and args[:4] == ["6", "2", "2", "2"]:
+            return "input+W0:conv", kn            # the 64-column bias conv over the s2d input
+        return CONV_LAYER.get((int(args[4]), int(args[5]))), kn
     if "input_stage_kernel" in name:
         return "input", name.split("(")[0].replace("void ", "")
+    if "s2d_input_kernel" in name:
+        return "input+W0:s2d", name.split("(")[0].replace("void ", "")
+    if "input_w0_kernel" in name:
+        return "input+W0:border", name.split("(")[0].replace("void ", "")
     if "final_q_kernel" in name or "final_stage_kernel" in name:
         return "final", name.split("(")[0]
     return None, None
