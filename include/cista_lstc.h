@@ -135,12 +135,13 @@ int cista_stage_output(const cista_config *cfg, const void *packed, int B, int h
                        const float *hstate, float *rec, float *pre_sigmoid, void *workspace,
                        size_t workspace_bytes, void *stream);
 
-/* ---- measurement hook (bench.py): launch exactly ONE kernel of the frame schedule on the
- * buffers of a previous cista_forward with the same io/workspace, so its duration can be
+/* ---- measurement hook (bench.py): launch ONE step of the frame schedule on the
+ * buffers of a previous cista_forward with the same io/workspace (CISTA_LAYER_INPUT: its 1-3
+ * kernels), so its duration can be
  * timed with events on `stream`.  Not a reference interface.  layer ids: */
 enum {
-    CISTA_LAYER_INPUT = 0,      /* We/Wi (VALU)                     */
-    CISTA_LAYER_W0 = 1,         /* stride-2 conv                    */
+    CISTA_LAYER_INPUT = 0,      /* We/Wi and W0 as one composed map (num_bins <= 8; x1 out) */
+    CISTA_LAYER_W0 = 1,         /* stride-2 conv; launches nothing when INPUT composed it */
     CISTA_LAYER_P0 = 2,
     CISTA_LAYER_GATES = 3,      /* ConvLSTC gates + cell update     */
     CISTA_LAYER_OUT_GATES = 4,
