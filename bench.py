@@ -328,7 +328,7 @@ def time_layers(torch, model, lib_mod, vox, B, H, W, device, reps):
         torch.cuda.synchronize()
     # the input stage computes W0 too (one composed linear map, input_w0_kernel): the W0 layer
     # launches nothing, so its work is credited to the fused launch
-    if "W0" in res and res["W0"]["ms"] < 0.05 * res["input"]["ms"]:
+    if "W0" in res and res["W0"]["ms"] < 0.25 * res["input"]["ms"]:   # unfused: W0 ~1.3x input
         w0 = res.pop("W0")
         res["input+W0"] = dict(res.pop("input"))
         r = res["input+W0"]
