@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define CISTA_ABI_VERSION 1
+#define CISTA_ABI_VERSION 2
 
 enum {
     CISTA_OK = 0,
@@ -105,6 +105,14 @@ int    cista_pack_params(const cista_config *cfg, const cista_params *params, vo
 
 /* scratch needed by cista_forward / the stage entries for one (B, H, W) */
 size_t cista_workspace_bytes(const cista_config *cfg, int B, int H, int W);
+
+/* Range flag.  The first int32 of every workspace (inference, training) is a sticky flag
+ * that the kernels set to 1 when an activation they split into fp16 hi/lo parts has
+ * |x| >= 65504 (or is inf): such a frame is not fp32-faithful.  The library never clears or
+ * reads it (no host sync): the caller zeroes it when it allocates the workspace (and after
+ * handling a report) and reads it asynchronously when it wants.  workspace bytes [0, 256)
+ * are reserved for it. */
+#define CISTA_RANGE_FLAG_OFFSET 0
 
 /* one recurrent frame for B independent sequences */
 int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int W,
@@ -182,6 +190,8 @@ typedef struct {
     float *g_z_prev;           /* out (B,h,w,2C)                                    */
     float *g_h_prev;           /* out (B,h,w,C)                                     */
     float *g_c_prev;           /* out (B,h,w,C)                                     */
+    float *g_events;           /* out (B,nb,H,W) NCHW; NULL = not needed (appended: */
+                               /* ABI version 2)                                    */
 } cista_grad_io;
 
 /* parameter gradients, same fields / layouts as cista_params; written (not accumulated) */

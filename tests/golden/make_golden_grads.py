@@ -7,6 +7,14 @@ g1: one frame with leaf previous states / previous image (requires_grad), loss =
     output times a fixed random tensor -> grads of all 25 parameters and of all 5 inputs.
 g2: train_e2v.py:108-120 semantics -- 3 frames, prev_img = output.clone() (no detach), states
     carried, loss = L1(last output, target) -> parameter grads (fp32 and fp64 reference).
+g3 (grads_180x240_seq15.npz): config c3's frame size and sequence length -- 180x240, 15 frames,
+    B=1, the g2 loss -> parameter grads of the fp32 reference and of the fp64 reference (stored
+    rounded to fp32), and the fp32-vs-fp64 noise of each (up to 2.3e-3: the 15-frame recurrence
+    amplifies fp32 rounding, so the GPU gradients are judged against the fp64 truth).  Its voxels
+    are NOT stored: tests regenerate them with oracle/fixtures.synthetic_voxels (seed below) and
+    check them against the stored checksum.
+
+    PYTHONPATH=/root/reference:. python tests/golden/make_golden_grads.py [g12] [g3]
 """
 from __future__ import annotations
 
@@ -19,6 +27,7 @@ import torch
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import fixtures as fx  # noqa: E402
+from tests.golden.g3_spec import G3, g3_inputs, g3_params  # noqa: E402
 from e2v.e2v_model import CistaLSTCNet  # noqa: E402
 
 torch.set_num_threads(8)
@@ -53,7 +62,8 @@ def main():
         leaves = [prev0.clone().requires_grad_(True), st0[0].clone().requires_grad_(True),
                   st0[1].clone().requires_grad_(True), st0[2][0].clone().requires_grad_(True),
                   st0[2][1].clone().requires_grad_(True)]
-        rec, st = m(torch.from_numpy(vox[1]).to(dtype), leaves[0], [leaves[1], leaves[2], (leaves[3], leaves[4])])
+        ev1 = torch.from_numpy(vox[1]).to(dtype).requires_grad_(True)       # the events' gradient too
+        rec, st = m(ev1, leaves[0], [leaves[1], leaves[2], (leaves[3], leaves[4])])
         outs = [rec, st[0], st[1], st[2][0], st[2][1]]
         if tag == "f32":
             Rs = [rng.standard_normal(o.shape).astype(np.float32) for o in outs]
@@ -69,6 +79,8 @@ def main():
         for i, n in enumerate(["prev_image", "c_lstc", "z", "h", "c"]):
             g = leaves[i].grad.detach().numpy()
             res[f"g1_{tag}_grad_{n}"] = g.astype(np.float32) if tag == "f32" else g
+        g = ev1.grad.detach().numpy()
+        res[f"g1_{tag}_grad_events"] = g.astype(np.float32) if tag == "f32" else g
         # ---------------- g2: 3-frame BPTT, L1 on the last frame -------------------------
         m = build(C, depth, params, dtype)
         target = torch.from_numpy(np.random.default_rng(6).uniform(0, 1, (B, 1, H, W))).to(dtype)
@@ -96,5 +108,43 @@ def main():
     print("wrote", os.path.join(HERE, "grads_32x48.npz"))
 
 
+def main_g3():
+    c = G3
+    params = g3_params()
+    vox, target = g3_inputs()
+    res = {"vox_sum": np.float64(vox.astype(np.float64).sum()),
+           "vox_abs_sum": np.float64(np.abs(vox.astype(np.float64)).sum())}
+    grads = {}
+    for dtype, tag in ((torch.float32, "f32"), (torch.float64, "f64")):
+        m = CistaLSTCNet([c["H"], c["W"]], base_channels=c["C"], depth=c["depth"], num_bins=5)
+        sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, c["depth"])
+        m.load_state_dict(sd, strict=True)
+        m = m.to(dtype)
+        prev = torch.zeros(c["B"], 1, c["H"], c["W"], dtype=dtype)
+        state = None
+        for s in range(c["L"]):
+            out, state = m(torch.from_numpy(vox[s]).to(dtype), prev, state)
+            prev = out.clone()
+        loss = torch.nn.functional.l1_loss(out, torch.from_numpy(target).to(dtype))
+        loss.backward()
+        res[f"{tag}_loss"] = np.float64(loss.item())
+        res[f"{tag}_last_frame"] = out.detach().double().numpy().astype(np.float32)
+        grads[tag] = unique_grads(m, c["depth"])
+    for k, v in grads["f32"].items():
+        res[f"f32_param_{k}"] = v.astype(np.float32)
+        v64 = grads["f64"][k]
+        res[f"f64_param_{k}"] = v64.astype(np.float32)       # the truth, rounded to fp32 (2^-24)
+        res[f"noise32_param_{k}"] = np.float64(np.abs(v - v64).max() / max(np.abs(v64).max(), 1e-30))
+    for k, v in c.items():
+        res[f"cfg_{k}"] = np.float64(v)
+    path = os.path.join(HERE, "grads_180x240_seq15.npz")
+    np.savez_compressed(path, **res)
+    print("wrote", path)
+
+
 if __name__ == "__main__":
-    main()
+    which = sys.argv[1:] or ["g12", "g3"]
+    if "g12" in which:
+        main()
+    if "g3" in which:
+        main_g3()

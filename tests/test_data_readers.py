@@ -74,3 +74,13 @@ def test_train_dataset_items(tmp_path):
     assert np.array_equal(events[: len(first)].numpy(), first.astype(np.float64))
     assert int(sizes.sum()) == events.shape[0]
     assert img.shape == (1, 24, 32) and img.dtype == torch.float32 and float(img.max()) <= 1.0
+
+
+def test_ragged_batch_refused_like_default_collate():
+    # a video's tail sequence (>= 5 reconstructions but < len_sequence) next to a full one:
+    # the reference's default collate raises; truncating would mislabel the full-length item
+    full = (torch.zeros(0, 4), torch.tensor([10] * 8), None, None)
+    tail = (torch.zeros(0, 4), torch.tensor([10] * 5), None, None)
+    assert data.GpuVoxelLoader.batch_length([full, full]) == 8
+    with pytest.raises(RuntimeError, match="equal size"):
+        data.GpuVoxelLoader.batch_length([full, tail])

@@ -1,9 +1,14 @@
 """BPTT backward of the HIP path against gradients produced by the
 real reference's autograd on CPU (tests/golden/make_golden_grads.py).
 
-Bar: max|hip - ref| / max|ref| <= 1e-3 per gradient tensor.  The reference's own fp32 gradients
-differ from its fp64 gradients by up to 5e-5 on these fixtures (stored as *_noise32_*), so the
-bar is 20x the reference's fp32 noise; the forward outputs keep the 1e-4 bar.
+Bars (max|hip - ref| / max|ref| per gradient tensor):
+  * 32x48 fixtures (g1, g2): GTOL = 2e-4 against the fp32 reference.  The reference's own fp32
+    gradients differ from its fp64 gradients by up to 4.8e-5 there (stored as *_noise32_*) and
+    the HIP gradients measured 4.8e-5 on MI355X, so the bar is ~4x either;
+  * c3 size (180x240, 15 frames, grads_180x240_seq15.npz): the fp32 reference itself is up to
+    2.3e-3 from the fp64 truth (the recurrence amplifies rounding), so the HIP gradients are held
+    against the fp64 truth: err(hip, f64) <= max(2 x err(ref fp32, f64), 1e-4) per tensor.
+The forward outputs keep the 1e-4 bar.
 """
 import numpy as np
 import pytest
@@ -15,7 +20,7 @@ from v2e2v_amd import CistaLSTCNet
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda"
-GTOL = 1e-3
+GTOL = 2e-4
 
 
 def model(C=64, depth=5):
@@ -41,7 +46,8 @@ def test_one_frame_all_gradients(golden):
     d = golden("grads_32x48.npz")
     m = model()
     leaves = [gpu(d["g1_prev_image"], True)] + [gpu(d[f"g1_prev_{n}"], True) for n in ("c_lstc", "z", "h", "c")]
-    rec, st = m(gpu(d["voxels"][1]), leaves[0], [leaves[1], leaves[2], (leaves[3], leaves[4])])
+    ev = gpu(d["voxels"][1], True)                   # the events' gradient (We dgrad) too
+    rec, st = m(ev, leaves[0], [leaves[1], leaves[2], (leaves[3], leaves[4])])
     outs = [rec, st[0], st[1], st[2][0], st[2][1]]
     loss = sum((o * gpu(d[f"g1_R{i}"])).sum() for i, o in enumerate(outs))
     loss.backward()
@@ -55,6 +61,9 @@ def test_one_frame_all_gradients(golden):
         e = rel_err(leaves[i].grad.detach().cpu().numpy(), d[f"g1_f32_grad_{n}"])
         if not e < GTOL:
             bad["input:" + n] = e
+    e = rel_err(ev.grad.detach().cpu().numpy(), d["g1_f32_grad_events"])
+    if not e < GTOL:
+        bad["input:events"] = e
     assert not bad, bad
 
 
@@ -112,3 +121,37 @@ def test_report_gradient_errors(golden, capsys):
         for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]:
             print(f"\n  grad {k:40s} hip-vs-ref32 {e:.2e}   ref32-vs-ref64 {n:.2e}", end="")
         print()
+
+
+def test_c3_size_bptt_against_fp64_truth(golden):
+    """Config c3's frame size and sequence length (train_e2v.py:108-130): 180x240, 15 frames,
+    prev_img = output.clone(), L1 on the last frame, one backward through the sequence."""
+    from tests.golden.g3_spec import G3, g3_inputs, g3_params
+    d = golden("grads_180x240_seq15.npz")
+    vox, target = g3_inputs()
+    assert float(vox.astype(np.float64).sum()) == float(d["vox_sum"])     # same inputs as the generator
+    c = G3
+    m = CistaLSTCNet([c["H"], c["W"]], base_channels=c["C"], depth=c["depth"], num_bins=5)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in g3_params().items()}, c["depth"])
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    prev = torch.zeros(c["B"], 1, c["H"], c["W"], device=DEV)
+    state = None
+    for s in range(c["L"]):
+        out, state = m(gpu(vox[s]), prev, state)
+        prev = out.clone()
+    loss = torch.nn.functional.l1_loss(out, gpu(target))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(out.detach().cpu().numpy(), d["f32_last_frame"]) < 1e-4
+    assert abs(loss.item() - float(d["f64_loss"])) <= 1e-4 * abs(float(d["f64_loss"]))
+    bad, rows = {}, []
+    for k, g in grads_by_name(m).items():
+        e = rel_err(g, d[f"f64_param_{k}"])
+        bar = max(2 * float(d[f"noise32_param_{k}"]), 1e-4)
+        rows.append((k, e, float(d[f"noise32_param_{k}"])))
+        if not e <= bar:
+            bad[k] = (e, bar)
+    print("\n" + "\n".join(f"  c3 grad {k:40s} hip-vs-f64 {e:.2e}   ref32-vs-f64 {n:.2e}"
+                            for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]))
+    assert not bad, bad

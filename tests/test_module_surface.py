@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 11
     for n in names:
         assert hasattr(L, n), n
-    assert L.cista_abi_version() == 1
+    assert L.cista_abi_version() == 2
     for s in range(6):
         assert L.cista_status_string(s)
 

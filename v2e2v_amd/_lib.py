@@ -49,7 +49,7 @@ LAYERS = ["input", "W0", "P0", "gates", "out_gates", "ista_D", "ista_P", "Dg", "
 class CistaGradIO(ctypes.Structure):
     _fields_ = [(n, c_void_p) for n in (
         "g_rec", "g_c_lstc", "g_z", "g_h", "g_c",
-        "g_prev_image", "g_c_lstc_prev", "g_z_prev", "g_h_prev", "g_c_prev")]
+        "g_prev_image", "g_c_lstc_prev", "g_z_prev", "g_h_prev", "g_c_prev", "g_events")]
 
 
 class CistaParamGrads(ctypes.Structure):

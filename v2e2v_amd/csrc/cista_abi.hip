@@ -5,6 +5,8 @@
 #include <stdint.h>
 #include <string.h>
 
+#include <mutex>
+
 #include "../../include/cista_lstc.h"
 #include "cista_kernels.hpp"
 #include "cista_backward.hpp"
@@ -99,14 +101,20 @@ struct Workspace {
     float *x1;     // (B,h,w,C)
     float *z0;     // (B,h,w,2C)
     float *xb;     // (B,h,w,C): ISTA x = x1 - D(z); later Dg output y
+    int *rflag;    // bytes [0, 4): the range flag (include/cista_lstc.h), caller-owned
     size_t bytes;
 };
+
+// every workspace (inference, training forward, backward) starts with this reserved header:
+// its first int32 is the range flag, which no carve hands out as scratch
+constexpr size_t WS_HEADER = ALIGN;
 
 Workspace carve(void *ws, int B, int H, int W, int C) {
     const size_t hw = (size_t)(H / 2) * (W / 2);
     Workspace w;
-    size_t off = 0;
+    size_t off = WS_HEADER;
     char *base = static_cast<char *>(ws);
+    w.rflag = reinterpret_cast<int *>(base);
     w.full = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * H * W * C * 4);
     w.x1 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * C * 4);
     w.z0 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * 2 * C * 4);
@@ -127,11 +135,11 @@ size_t lds_bytes(int TH, int TW, int S) {
 
 // max_items: staging items (HP rounded to 8, x4 k-groups) one workgroup may hold in registers
 // (0 = unlimited); nbuf: LDS images (2 for the double-buffered loop)
-Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf) {
+Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ = 2) {
     Tile best{1, 1, Hout, Wout, 0};
     double best_eff = -1.0;
     size_t best_lds = ~(size_t)0;
-    const size_t lds_cap = 80 * 1024;   // two workgroups per CU
+    const size_t lds_cap = 160 * 1024 / occ;   // occ workgroups per CU
     for (int TW = 1; TW <= block_px && TW <= Wout; ++TW) {
 #if CISTA_TW16
         // 16-pixel m-tiles that never wrap a tile row read LDS without bank conflicts
@@ -156,26 +164,29 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
     return best;
 }
 
-// dynamic LDS above 64 KiB must be enabled per kernel (once; not a stream operation)
+// dynamic LDS above 64 KiB must be enabled per kernel (once; not a stream operation).  The
+// ABI is reentrant: host threads launching concurrently share this table under a lock.
 bool allow_big_lds(const void *kern) {
-    static const void *done[64];
+    static std::mutex mu;
+    static const void *done[128];
     static int ndone = 0;
+    std::lock_guard<std::mutex> lock(mu);
     for (int i = 0; i < ndone; ++i)
         if (done[i] == kern) return true;
     if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
         return false;
-    if (ndone < 64) done[ndone++] = kern;
+    if (ndone < 128) done[ndone++] = kern;
     return true;
 }
 
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
-    const Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1);
+    const Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC);
     a.TH = t.TH;
     a.TW = t.TW;
     a.tiles_y = t.ty;
@@ -184,9 +195,10 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
     // the training variant (SV) only for epilogues that save activations, and only when asked
     constexpr bool HAS_SV = EPI == EPI_ISTA_P || EPI == EPI_LSTC_CELL || EPI == EPI_LSTC_OUT || EPI == EPI_LSTM;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false>;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false, OCC>;
     if constexpr (HAS_SV)
-        if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr) kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true>;
+        if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr)
+            kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
 #if CISTA_XCD
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
@@ -323,6 +335,7 @@ struct Frame {
     float *lg;             // ConvLSTM gates (i, r, o, g) post-activation (B,h,w,4C)
     float *u;              // relu(upsamp_conv(...))                      (B,H,W,C)
     bool need_full;        // the input stage must write x_full (the backward's recompute)
+    int *rflag;            // range flag (workspace header)
     hipStream_t st;
 };
 
@@ -339,6 +352,13 @@ inline bool s2d_input(const cista_config &cfg) { return CISTA_S2D_IN && cfg.num_
 
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
+
+ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int Hout, int Wout,
+                     const float *in0, int c0, const float *in1, int c1) {
+    ConvArgs a = conv_args(f.packed, f.L, id, C, B, Hin, Win, Hout, Wout, in0, c0, in1, c1);
+    a.rflag = f.rflag;
+    return a;
+}
 
 int run_layer(const Frame &f, int layer, int it = 0) {
     const size_t hw = (size_t)f.B * f.h * f.w;
@@ -367,7 +387,7 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                         NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7)
 #undef NBCASE
                     }
-                    a = conv_args(f.packed, f.L, CV_IN, C, B, h, w, h, w, f.full, 32, nullptr, 0);
+                    a = conv_args_f(f, CV_IN, C, B, h, w, h, w, f.full, 32, nullptr, 0);
                     a.out0 = f.x1;
                     if (const int sc = launch_conv<STAGE_S1, EPI_BIAS, 1>(a, f.st)) return sc;
                     fa.border_only = 1;
@@ -413,42 +433,42 @@ int run_layer(const Frame &f, int layer, int it = 0) {
         }
         case CISTA_LAYER_W0:                                           // e2v_model.py:66
             if (fused_input(*f.cfg) && !f.need_full) return CISTA_OK;  // done by the input stage
-            a = conv_args(f.packed, f.L, CV_W0, C, B, f.H, f.W, h, w, f.full, C, nullptr, 0);
+            a = conv_args_f(f, CV_W0, C, B, f.H, f.W, h, w, f.full, C, nullptr, 0);
             a.out0 = f.x1;
             return launch_conv<STAGE_S2, EPI_BIAS, 1>(a, f.st);
         case CISTA_LAYER_P0:                                           // base_layers.py:61
-            a = conv_args(f.packed, f.L, CV_P0, C, B, h, w, h, w, f.x1, C, nullptr, 0);
+            a = conv_args_f(f, CV_P0, C, B, h, w, h, w, f.x1, C, nullptr, 0);
             a.out0 = f.z0;
             return launch_conv<STAGE_S1, EPI_BIAS, 1>(a, f.st);
         case CISTA_LAYER_GATES:     // c = sig(f) c_prev + sig(i) z0, gates(cat(x1, z_prev)) :57-67
-            a = conv_args(f.packed, f.L, CV_GATES, C, B, h, w, h, w, f.x1, C, f.z_prev, 2 * C);
+            a = conv_args_f(f, CV_GATES, C, B, h, w, h, w, f.x1, C, f.z_prev, 2 * C);
             a.out0 = f.c_lstc; a.aux0 = f.c_lstc_prev; a.aux1 = f.z0;
             a.out1 = f.gi; a.out2 = f.gf;
             return launch_conv<STAGE_S1, EPI_LSTC_CELL, 2>(a, f.st);
         case CISTA_LAYER_OUT_GATES: // z = sig(out_gates(cat(z0, z_prev))) tanh(c)          :63,69
-            a = conv_args(f.packed, f.L, CV_OUTG, C, B, h, w, h, w, f.z0, 2 * C, f.z_prev, 2 * C);
+            a = conv_args_f(f, CV_OUTG, C, B, h, w, h, w, f.z0, 2 * C, f.z_prev, 2 * C);
             a.out0 = (f.zl && f.cfg->depth > 0) ? f.zl : f.z; a.aux0 = f.c_lstc; a.out1 = f.go;
             return launch_conv<STAGE_S1, EPI_LSTC_OUT, 1>(a, f.st);
         case CISTA_LAYER_ISTA_D:    // x = x1 - D(z)                              e2v_model.py:73-74
-            a = conv_args(f.packed, f.L, CV_D, C, B, h, w, h, w, zl_in ? f.zl : f.z, 2 * C, nullptr, 0);
+            a = conv_args_f(f, CV_D, C, B, h, w, h, w, zl_in ? f.zl : f.z, 2 * C, nullptr, 0);
             a.out0 = f.xs ? f.xs + it * hw * C : f.xb; a.aux0 = f.x1;
             return launch_conv<STAGE_S1, EPI_ISTA_D, 1>(a, f.st);
         case CISTA_LAYER_ISTA_P:    // z = softshrink(P(x) + z, lambda)            :75-77
-            a = conv_args(f.packed, f.L, CV_P, C, B, h, w, h, w, f.xs ? f.xs + it * hw * C : f.xb, C,
+            a = conv_args_f(f, CV_P, C, B, h, w, h, w, f.xs ? f.xs + it * hw * C : f.xb, C,
                           nullptr, 0);
             a.out0 = f.z; a.aux0 = zl_in ? f.zl : f.z; a.lambda = blob<float>(f.packed, f.L.lambda);
             a.out1 = f.v ? f.v + it * hw * 2 * C : nullptr;
             return launch_conv<STAGE_S1, EPI_ISTA_P, 1>(a, f.st);
         case CISTA_LAYER_DG:        // y = relu(Dg.conv(z))                      base_layers.py:222
-            a = conv_args(f.packed, f.L, CV_DG, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
+            a = conv_args_f(f, CV_DG, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
             a.out0 = f.y ? f.y : f.xb;
             return launch_conv<STAGE_S1, EPI_RELU, 1>(a, f.st);
         case CISTA_LAYER_LSTM:      // ConvLSTM on cat(y, h_prev)                  :112-128
-            a = conv_args(f.packed, f.L, CV_LSTM, C, B, h, w, h, w, f.y ? f.y : f.xb, C, f.h_prev, C);
+            a = conv_args_f(f, CV_LSTM, C, B, h, w, h, w, f.y ? f.y : f.xb, C, f.h_prev, C);
             a.out0 = f.hs; a.out1 = f.cs; a.aux0 = f.c_prev; a.out2 = f.lg;
             return launch_conv<STAGE_S1, EPI_LSTM, 4>(a, f.st);
         case CISTA_LAYER_UPSAMPLE:  // relu(conv(ReflectionPad(up2x(h))))          :193-210
-            a = conv_args(f.packed, f.L, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
+            a = conv_args_f(f, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
             a.out0 = f.full;
             if (up_q_path(C)) {     // + final_conv's channel contraction in the epilogue
                 a.aux0 = blob<float>(f.packed, f.L.wF);
@@ -485,7 +505,7 @@ Frame make_frame(const cista_config *cfg, const void *packed, int B, int H, int 
     f.cfg = cfg; f.packed = packed; f.L = make_layout(*cfg);
     f.B = B; f.H = H; f.W = W; f.h = H / 2; f.w = W / 2; f.C = cfg->base_channels;
     const Workspace wsp = carve(ws, B, H, W, f.C);
-    f.full = wsp.full; f.x1 = wsp.x1; f.z0 = wsp.z0; f.xb = wsp.xb;
+    f.full = wsp.full; f.x1 = wsp.x1; f.z0 = wsp.z0; f.xb = wsp.xb; f.rflag = wsp.rflag;
     f.st = static_cast<hipStream_t>(stream);
     return f;
 }
@@ -587,7 +607,7 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     const int h = H / 2, w = W / 2, C = cfg.base_channels;
     const size_t hw = (size_t)B * h * w, HW = (size_t)B * H * W;
     BwdWs s;
-    size_t off = 0;
+    size_t off = WS_HEADER;    // the range flag survives the backward's use of the buffer
     char *base = static_cast<char *>(buf);
     auto take = [&](size_t nfloat) {
         float *p = reinterpret_cast<float *>(base + off);
@@ -967,6 +987,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.mask = nullptr; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = half;
         d.Cin = 1; d.accumulate = 0;
         hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW), dim3(256), 0, st, d);
+    }
+    if (g.g_events) {                            // We dgrad: the events' own gradient
+        DgradSmallArgs d;
+        d.G = gxfull; d.Gc = C; d.Goff = 0; d.W = P.We_w; d.dX = g.g_events; d.Xc = 0; d.Xoff = 0;
+        d.mask = nullptr; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = half;
+        d.Cin = nb; d.accumulate = 0;
+        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * nb), dim3(256), 0, st, d);
     }
     return hip_ok();
 }

@@ -728,7 +728,7 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *parti
 // generic VALU dgrad of a small reflect-padded 3x3 conv with stride S (W0, final_conv, Wi):
 // dX[b,Q,ci] (+)= sum over (P, t) with reflect(S*P + t - 1) == Q of G[b,P,co] W[co][ci][t]
 // G NHWC (B, Hout, Wout, Gc) channels [Goff, Goff+Cout); dX layout NHWC (Xc, Xoff) or, for
-// Xc == 0, NCHW planes with Cin == 1 (prev_image).
+// Xc == 0, NCHW planes (prev_image: Cin == 1; events: Cin == num_bins).
 // --------------------------------------------------------------------------------------------
 struct DgradSmallArgs {
     const float *G; int Gc, Goff;
@@ -787,7 +787,8 @@ __global__ __launch_bounds__(256) void dgrad_small_kernel(const DgradSmallArgs a
                 for (int co = 0; co < a.Cout; ++co) s = fmaf(g[co], a.W[((size_t)co * a.Cin + ci) * 9 + t], s);
             }
         }
-    const size_t o = a.Xc ? (size_t)pix * a.Xc + a.Xoff + ci : (size_t)pix;
+    const size_t o = a.Xc ? (size_t)pix * a.Xc + a.Xoff + ci
+                          : ((size_t)b * a.Cin + ci) * a.Hin * a.Win + (size_t)y * a.Win + x;
     if (a.accumulate) s += a.dX[o];
     if (a.mask && !(a.mask[o] > 0.0f)) s = 0.0f;
     a.dX[o] = s;
@@ -996,7 +997,7 @@ __global__ void softshrink_fwd_kernel(const float *v, const float *lam, float *z
     const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= npix * C) return;
     const float x = v[i], l = lam[i % C];
-    z[i] = fmaxf(x - l, 0.0f) - fmaxf(-x - l, 0.0f);
+    z[i] = softshrink_(x, l);
 }
 
 // ConvLSTC cell backward (reference base_layers.py:52-71), per (pixel, channel), Cz = 2C:

@@ -99,6 +99,7 @@ struct ConvArgs {
     //   4*Cout channels in the reference gate order; EPI_UP_Q: out1 = u = relu(acc + b)
     float *out2;
     const float *ascale; // optional [2]: {s, 1/s} power-of-two input pre-scale (dgrad inputs)
+    int *rflag;          // optional: set to 1 when a staged |x| >= 65504 (fp16 split range)
 };
 
 __device__ __forceinline__ int reflect_clamp(int i, int n) {
@@ -112,8 +113,14 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
-// split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25)
-__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo) {
+// torch.relu: NaN stays NaN (fmaxf alone would map it to 0 and hide an upstream overflow)
+__device__ __forceinline__ float relu_(float x) { return x != x ? x : fmaxf(x, 0.0f); }
+// reference softshrink formula, base_layers.py:11-12: relu(x - l) - relu(-x - l)
+__device__ __forceinline__ float softshrink_(float x, float l) { return relu_(x - l) - relu_(-x - l); }
+
+// split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25); amax
+// tracks the largest staged magnitude: >= 65504 does not fit the fp16 hi part (range flag)
+__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, float &amax) {
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     f16x8 h, l;
 #pragma unroll
@@ -121,6 +128,7 @@ __device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &
         const _Float16 hb = (_Float16)v[i];
         h[i] = hb;
         l[i] = (_Float16)(v[i] - (float)hb);
+        amax = fmaxf(amax, fabsf(v[i]));
     }
     hi = __builtin_bit_cast(u32x4, h);
     lo = __builtin_bit_cast(u32x4, l);
@@ -199,7 +207,7 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
 template <int STAGE>
 __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
                                             int ix0, int HH, int HWd, int HPpad,
-                                            const float *seg, int segC, int choff) {
+                                            const float *seg, int segC, int choff, float &amax) {
     constexpr int BATCH = STAGE == STAGE_UP ? 2 : 4;
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
@@ -219,7 +227,7 @@ __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int 
         for (int u = 0; u < BATCH; ++u) {
             if (hps[u] < 0) continue;
             u32x4 hi, lo;
-            split8(v0[u], v1[u], hi, lo);
+            split8(v0[u], v1[u], hi, lo, amax);
             smem[gs[u] * HPpad + hps[u]] = hi;
             smem[(4 + gs[u]) * HPpad + hps[u]] = lo;
         }
@@ -250,12 +258,12 @@ __device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, i
 template <int NI>
 __device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4 (&v0)[NI],
                                              const float4 (&v1)[NI], const int (&hps)[NI],
-                                             const int (&gs)[NI]) {
+                                             const int (&gs)[NI], float &amax) {
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         if (hps[u] < 0) continue;
         u32x4 hi, lo;
-        split8(v0[u], v1[u], hi, lo);
+        split8(v0[u], v1[u], hi, lo, amax);
         buf[gs[u] * HPpad + hps[u]] = hi;
         buf[(4 + gs[u]) * HPpad + hps[u]] = lo;
     }
@@ -351,8 +359,10 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
 // ------------------------------------------------------------------------------------------
 // SV: training variant -- the epilogue also stores the activations the BPTT backward needs
 // (out1 / out2, see ConvArgs); the inference variant has no such stores in its epilogue.
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false>
-__global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
+// OCC: workgroups per CU the register budget is sized for (LDS: the host's tile choice)
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false,
+          int OCC = 2>
+__global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     // NI > 0: double-buffered K loop (two LDS images, next chunk's loads in NI x 8 VGPRs)
     static_assert(WM * WN == 4, "4 waves per workgroup");
     static_assert(NW % G == 0, "a wave must hold whole gate groups");
@@ -412,6 +422,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+    float amax = 0.0f;   // largest staged |x| of this thread (range flag, see ConvArgs.rflag)
     const int NT = a.N >> 4;
     const int nt0 = (nblk * WN + wn) * NW;
     const int kc0 = a.c0 >> 5;
@@ -434,7 +445,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
             seg_of(0, seg, segC, choff);
             float4 sv0[NI], sv1[NI];
             stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1);
-            stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg);
+            stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
         }
         __syncthreads();
         for (int kc = 0; kc < nchunks; ++kc) {
@@ -483,7 +494,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                     }
                 }
             }
-            if (more && !CISTA_EXP_NOSTAGE) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg);
+            if (more && !CISTA_EXP_NOSTAGE) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg, amax);
             __syncthreads();
         }
     } else
@@ -491,7 +502,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
         __syncthreads();
-        stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff);
+        stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff, amax);
         __syncthreads();
 
         const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
@@ -541,6 +552,9 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
         }
     }
 
+    // an activation beyond the fp16 range of the hi part (or inf): the result is not fp32-faithful
+    if (amax >= 65504.0f && a.rflag) *a.rflag = 1;
+
     // ---------------------------------- epilogue ----------------------------------------
     // acc[m][n][j]: pixel row (wm*MT_W+m)*16 + 4*(lane>>4) + j, packed column (nt0+n)*16 + lane&15
     const int col = lane & 15;
@@ -575,7 +589,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                 const float *wf = wfs + (nt0 + n) * 16 + col;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
-                    const float u = fmaxf(acc[m][n][j] + bz[n], 0.0f);
+                    const float u = relu_(acc[m][n][j] + bz[n]);
                     if constexpr (EPI == EPI_UP_Q_SAVE) {   // keep u for the final_conv / ReLU backward
                         const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
                         const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
@@ -715,7 +729,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                     const float *vv = reinterpret_cast<const float *>(v);
                     if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? fmaxf(vv[e], 0.0f) : vv[e];
+                        for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? relu_(vv[e]) : vv[e];
                     } else if constexpr (EPI == EPI_ISTA_D) {
                         const float4 x1 = curA0[it0 / 64];
                         const float *xx = reinterpret_cast<const float *>(&x1);
@@ -729,7 +743,7 @@ __global__ __launch_bounds__(256, 2) void conv3x3_split3(const ConvArgs a) {
                         for (int e = 0; e < 4; ++e) {
                             const float x = vv[e] + zz[e];
                             r1[e] = x;
-                            r[e] = fmaxf(x - ll[e], 0.0f) - fmaxf(-x - ll[e], 0.0f);
+                            r[e] = softshrink_(x, ll[e]);
                         }
                         if constexpr (SV)
                             if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);

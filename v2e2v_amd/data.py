@@ -213,9 +213,22 @@ class GpuVoxelLoader:
     def __len__(self):
         return len(self.loader)
 
+    @staticmethod
+    def batch_length(items):
+        """Sequence length of a batch.  split_sequences keeps a video's tail sequence when it
+        has enough reconstructions, so lengths can differ; the reference's default collate
+        refuses such a batch (torch default_collate: 'each element in list of batch should be
+        of equal size'), and so does this loader -- truncating would pair the full-length items'
+        frames with a ground truth from a later window."""
+        lens = {len(it[1]) for it in items}
+        if len(lens) != 1:
+            raise RuntimeError(f"each element in list of batch should be of equal size (sequence "
+                               f"lengths {sorted(lens)} in one batch)")
+        return lens.pop()
+
     def __iter__(self):
         for items in self.loader:
-            L = min(len(it[1]) for it in items)
+            L = self.batch_length(items)
             evs, sizes = [], []
             for s in range(L):                       # window order: (step, sequence)
                 for events, sz, _, _ in items:

@@ -48,6 +48,7 @@ class CistaLSTCNet(nn.Module):
         self._packed = None
         self._packed_key = None
         self._ws = None
+        self.range_check = True      # asynchronous fp16-range guard (check_numerics())
 
     # ------------------------------------------------------------------ internals
     def _cfg(self):
@@ -76,6 +77,8 @@ class CistaLSTCNet(nn.Module):
         if dev.type != "cuda":
             raise RuntimeError("CistaLSTCNet (MI355X build) runs on ROCm devices only; move the "
                                "module to 'cuda' (the CPU restatement is test-only: oracle/)")
+        # in-place updates through autograd-visible ops (optimizer steps, copy_ under no_grad)
+        # bump _version; writes through `.data` do not -- call invalidate_packed() after those
         key = tuple((p.data_ptr(), p._version) for p in params)
         if self._packed is not None and self._packed_key == key:
             return self._packed
@@ -91,12 +94,64 @@ class CistaLSTCNet(nn.Module):
         self._packed, self._packed_key = packed, key
         return packed
 
+    def invalidate_packed(self):
+        """Drop the packed split-fp16 weights: the next forward repacks.  Needed after writing
+        parameters through ``.data`` (e.g. ``Lambda.data.clamp_(min=0)``), which PyTorch does
+        not version-count; load_state_dict and .to()/.cuda() invalidate automatically."""
+        self._packed = None
+        self._packed_key = None
+
+    def _load_from_state_dict(self, *args, **kwargs):
+        self.invalidate_packed()
+        return super()._load_from_state_dict(*args, **kwargs)
+
+    def _apply(self, fn, *args, **kwargs):
+        self.invalidate_packed()
+        self._ws = None
+        self._tws = None
+        return super()._apply(fn, *args, **kwargs)
+
     def workspace(self, B, H, W, device):
         L = _lib.lib()
         n = L.cista_workspace_bytes(ctypes_ref(self._cfg()), B, H, W)
         if self._ws is None or self._ws.numel() < n or self._ws.device != device:
             self._ws = torch.empty(n, dtype=torch.uint8, device=device)
+            self._ws[:_RANGE_HDR].zero_()                 # the range flag (cista_lstc.h)
         return self._ws
+
+    # ---------------------------------------------------------------- numerics guard
+    def _range_poll(self, ws):
+        """Asynchronous range check (include/cista_lstc.h, range flag): raises if a previous
+        frame staged an activation the split-fp16 MFMA path cannot represent (|x| >= 65504).
+        No host sync: the flag is copied to pinned memory behind the frame's kernels and looked
+        at once that copy has completed (a report arrives a frame or two late)."""
+        st = self.__dict__.setdefault("_range_state", {})
+        slot = st.get(id(ws))
+        if slot is None:            # [pinned host int32, event, copy in flight]
+            slot = st[id(ws)] = [torch.zeros(1, dtype=torch.int32, pin_memory=True), torch.cuda.Event(), False]
+        if slot[2] and slot[1].query():
+            slot[2] = False
+            if int(slot[0][0]) != 0:
+                slot[0].zero_()
+                ws[:_RANGE_HDR].zero_()
+                raise _lib.CistaError(_RANGE_MSG)
+        if not slot[2]:
+            slot[0].copy_(ws[:4].view(torch.int32), non_blocking=True)
+            slot[1].record(torch.cuda.current_stream(ws.device))
+            slot[2] = True
+
+    def check_numerics(self):
+        """Synchronous form of the range check over every frame run since the last call."""
+        for ws in (self._ws, getattr(self, "_tws", None)):
+            if ws is None:
+                continue
+            flag = int(ws[:4].view(torch.int32).item())
+            ws[:_RANGE_HDR].zero_()
+            slot = self.__dict__.get("_range_state", {}).pop(id(ws), None)
+            if slot is not None and slot[2]:
+                slot[1].synchronize()
+            if flag:
+                raise _lib.CistaError(_RANGE_MSG)
 
     # ------------------------------------------------------------------ forward
     def forward(self, events, prev_image, prev_states):
@@ -114,8 +169,14 @@ class CistaLSTCNet(nn.Module):
         ws = getattr(self, "_tws", None)
         if ws is None or ws.numel() < n or ws.device != device:
             ws = torch.empty(n, dtype=torch.uint8, device=device)
+            ws[:_RANGE_HDR].zero_()
             self._tws = ws
         return ws
+
+
+_RANGE_HDR = 256       # workspace header holding the range flag (CISTA_RANGE_FLAG_OFFSET)
+_RANGE_MSG = ("CistaLSTCNet: an activation reached |x| >= 65504 (or inf), beyond the range of the "
+              "split-fp16 MFMA path; the frame is not fp32-faithful (DESIGN.md section 5)")
 
 
 def ctypes_ref(x):
@@ -179,6 +240,8 @@ def _forward_frame(model, events, prev_image, prev_states):
     _lib.check(L.cista_forward(ctypes_ref(model._cfg()), packed.data_ptr(), B, H, W,
                                ctypes_ref(io), ws.data_ptr(), ws.numel(),
                                _lib.stream_handle(dev)), "cista_forward")
+    if model.range_check:
+        model._range_poll(ws)
     return rec, [c_lstc, z, (hs, cs)]
 
 
@@ -231,6 +294,7 @@ class _CistaFrame(torch.autograd.Function):
         return rec, c_lstc, z, hs, cs
 
     @staticmethod
+    @torch.autograd.function.once_differentiable
     def backward(ctx, g_rec, g_cl, g_z, g_h, g_c):
         model = ctx.model
         ev, pi, clp, zp, hp, cp, rec, c_lstc, z, hs, cs, saved = ctx.saved_tensors
@@ -243,6 +307,7 @@ class _CistaFrame(torch.autograd.Function):
         g_rec = None if g_rec is None else g_rec.float().contiguous()
         g_cl, g_z, g_h, g_c = _cl(g_cl), _cl(g_z), _cl(g_h), _cl(g_c)
         need = ctx.needs_input_grad
+        g_ev = torch.empty_like(ev) if need[1] else None
         g_pi = torch.empty_like(pi) if need[2] else None
         g_clp = torch.empty_like(clp, memory_format=torch.channels_last) if (clp is not None and need[3]) else None
         g_zp = torch.empty_like(zp, memory_format=torch.channels_last) if (zp is not None and need[4]) else None
@@ -252,7 +317,7 @@ class _CistaFrame(torch.autograd.Function):
         P = _lib.ptr
         io = _lib.CistaFrameIO(P(ev), P(pi), P(clp), P(zp), P(hp), P(cp), P(rec), P(c_lstc), P(z), P(hs), P(cs))
         gio = _lib.CistaGradIO(P(g_rec), P(g_cl), P(g_z), P(g_h), P(g_c), P(g_pi), P(g_clp), P(g_zp),
-                               P(g_hp), P(g_cp))
+                               P(g_hp), P(g_cp), P(g_ev))
         cp_ = _lib.CistaParams(*[t.data_ptr() for t in params])
         pg = _lib.CistaParamGrads(*[t.data_ptr() for t in pgrads])
         ws = model.train_workspace(B, H, W, dev)
@@ -262,7 +327,7 @@ class _CistaFrame(torch.autograd.Function):
                                     _lib.stream_handle(dev)), "cista_backward")
         # keep the host-side argument tensors alive until the stream has consumed them
         model._bwd_keepalive = (params, g_rec, g_cl, g_z, g_h, g_c)
-        return (None, None, g_pi, g_clp, g_zp, g_hp, g_cp, *pgrads)
+        return (None, g_ev, g_pi, g_clp, g_zp, g_hp, g_cp, *pgrads)
 
 
 def _train_frame(model, events, prev_image, prev_states):
@@ -288,4 +353,6 @@ def _train_frame(model, events, prev_image, prev_states):
     if (sts[2] is None) != (sts[3] is None):
         raise RuntimeError("prev_states[2] must be None or an (h, c) pair")
     rec, c_lstc, z, hs, cs = _CistaFrame.apply(model, events, prev_image, *sts, *model._unique_params())
+    if model.range_check:
+        model._range_poll(model.train_workspace(B, H, W, dev))
     return rec, [c_lstc, z, (hs, cs)]
