@@ -36,7 +36,15 @@ extern "C" {
 enum {
     CISTA_VOXEL_RAW = 0,     /* no normalisation (events_to_voxel_grid output)                 */
     CISTA_VOXEL_STD = 1,     /* mode='std': mean/std of the non-zero voxels -> (0, 1)          */
-    CISTA_VOXEL_MAXMIN = 2   /* mode='maxmin': (v - min) / (max - min + 1e-8)                  */
+    CISTA_VOXEL_MAXMIN = 2,  /* mode='maxmin': (v - min) / (max - min + 1e-8)                  */
+    CISTA_VOXEL_STD_F32 = 3, /* mode='std' of event_preprocess_pytorch (:157-176): float32
+                                scalars and elementwise math, as torch computes them (the sums
+                                rounded once to float32; ATen's reduction order may differ in
+                                the last bit of sum())                                          */
+    CISTA_VOXEL_TORCH_ACCUM = 0x10  /* cista_voxelize flag: accumulate like
+                                events_to_voxel_grid_pytorch (:66-129): float32 contributions
+                                and float32 index_add_ (bit-identical to the reference on a
+                                float64 events tensor) instead of numpy's np.add.at           */
 };
 
 /* Workspace for cista_voxelize: n_events = total events of the batch (offsets[B]). */

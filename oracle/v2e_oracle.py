@@ -3,12 +3,17 @@
 :158-253, IIR_temporal_filtering :266-289) and v2e/emulator_utils.py:13-207 (lin_log,
 rescale_intensity_frame, low_pass_filter, subtract_leak_current, generate_shot_noise).
 
-PARITY UNPINNED: the reference emulator cannot be imported here (v2e_model.py imports cv2 and
-matplotlib, both absent) and no reference fixture exercises it.  Its random draws
-(torch.normal / randn / rand) make parity statistical anyway; this restatement takes the random
-arrays from a pluggable source so the deterministic configuration (sigma_thres = 0,
-leak_rate_hz = 0, shot_noise_rate_hz = 0) can be compared value for value.  Only tests/ import
-this module.
+Parity: the emulator's forward (v2e_model.py:290-536) cannot be imported here (the module
+imports cv2 and matplotlib, both absent), so the composition below is restated, not
+executed from the reference.  Its BUILDING BLOCKS are pinned: lin_log, rescale_intensity_frame,
+low_pass_filter, subtract_leak_current, compute_event_map (v2e/emulator_utils.py) and the torch
+voxel twins events_to_voxel_grid_pytorch / event_preprocess_pytorch (utils/event_process.py)
+are checked against vectors the real reference functions produced
+(tests/golden/make_golden_v2e.py -> v2e_blocks.npz; tests/test_oracle_v2e_golden.py).  The
+random draws (torch.normal / randn / rand) make whole-forward parity statistical anyway; this
+restatement takes the random arrays from a pluggable source so the deterministic configuration
+(sigma_thres = 0, leak_rate_hz = 0, shot_noise_rate_hz = 0) can be compared value for value.
+Only tests/ import this module.
 """
 from __future__ import annotations
 
@@ -44,6 +49,104 @@ def torch_linspace_f32(start, end, steps):
 def rescale_intensity_frame(x):
     """emulator_utils.py:41-46."""
     return ((x + f32(20)) / f32(275)).astype(f32)
+
+
+def low_pass_filter(log_new, lp0, inten01, dt, cutoff_hz, ql=1.0, qs=1.0):
+    """emulator_utils.py:49-101: first-order intensity-dependent IIR; the (0::2, 0::2) pixels
+    use the qs time constant.  float32 like the reference's tensors (dt a float32 scalar)."""
+    if cutoff_hz <= 0:
+        return log_new
+    inten01 = inten01.astype(f32)
+    if ql > 0:
+        tau0 = 1 / (math.pi * 2 * cutoff_hz * ql)
+        eps = (inten01 * (f32(dt) / f32(tau0))).astype(f32)
+    else:
+        eps = np.ones_like(inten01)
+    if qs > 0:
+        tau1 = 1 / (math.pi * 2 * cutoff_hz * qs)
+        eps1 = (inten01 * (f32(dt) / f32(tau1))).astype(f32)
+        eps[:, :, 0::2, 0::2] = eps1[:, :, 0::2, 0::2]
+    else:
+        eps[:, :, 0::2, 0::2] = 1
+    eps = np.minimum(eps, f32(1))
+    return ((f32(1) - eps) * lp0 + eps * log_new).astype(f32)
+
+
+def subtract_leak_current(base, leak_rate_hz, dt, pos_thres, leak_jitter_fraction, noise_rate, rand):
+    """emulator_utils.py:104-126; `rand` is the standard-normal draw (torch.randn there)."""
+    cur = (f32(leak_rate_hz) * noise_rate * (f32(1) - f32(leak_jitter_fraction) * rand)).astype(f32)
+    return (base - (f32(dt) * cur).astype(f32) * pos_thres).astype(f32)
+
+
+def _div_floor(a, b):
+    """ATen's float floor division (torch.div(..., rounding_mode='floor')): Python semantics via
+    fmod, not floor(a / b)."""
+    a, b = a.astype(f32), b.astype(f32)
+    mod = np.fmod(a, b)
+    div = ((a - mod) / b).astype(f32)
+    div = np.where((mod != 0) & ((b < 0) != (mod < 0)), div - f32(1), div).astype(f32)
+    fl = np.floor(div)
+    fl = np.where(div - fl > f32(0.5), fl + f32(1), fl)
+    return np.where(div != 0, fl, np.copysign(f32(0), a / b)).astype(f32)
+
+
+def compute_event_map(diff, pos_thres, neg_thres):
+    """emulator_utils.py:129-162: ON / OFF event counts of a log-intensity difference."""
+    pos = np.maximum(diff, f32(0)).astype(f32)
+    neg = np.maximum(-diff, f32(0)).astype(f32)
+    return _div_floor(pos, pos_thres).astype(np.int32), _div_floor(neg, neg_thres).astype(np.int32)
+
+
+def events_to_voxel_grid_pytorch(events, num_bins, width, height):
+    """utils/event_process.py:66-129 with a float64 events tensor: timestamps normalised in
+    float64, the contributions rounded to float32 (`dts.float()`, float32 polarities), and
+    index_add_ on the float32 grid adding them in event order, left contributions first."""
+    vox = np.zeros(num_bins * height * width, f32)
+    if len(events) == 0:
+        return vox.reshape(num_bins, height, width)
+    t = events[:, 0].astype(np.float64)
+    dT = t[-1] - t[0]
+    if dT == 0:
+        dT = 1.0
+    ts = (num_bins - 1) * (t - t[0]) / dT
+    xs = events[:, 1].astype(np.int64)
+    ys = events[:, 2].astype(np.int64)
+    pol = events[:, 3].astype(f32).copy()
+    pol[pol == 0] = -1
+    tis = np.floor(ts)
+    dts = (ts - tis).astype(f32)
+    vl = (pol * (f32(1) - dts)).astype(f32)
+    vr = (pol * dts).astype(f32)
+    ti = tis.astype(np.int64)
+    ok = (tis < num_bins) & (tis >= 0)
+    np.add.at(vox, xs[ok] + ys[ok] * width + ti[ok] * width * height, vl[ok])
+    ok = ((tis + 1) < num_bins) & (tis >= 0)
+    np.add.at(vox, xs[ok] + ys[ok] * width + (ti[ok] + 1) * width * height, vr[ok])
+    return vox.reshape(num_bins, height, width)
+
+
+def event_preprocess_pytorch(vox, mode="std", filter_hot_pixel=True):
+    """utils/event_process.py:157-176 in float32 torch semantics: sum() is a float32 scalar
+    (here the exact sum rounded once to float32; ATen's own reduction order may differ in the
+    last bits), `/ num_nonzeros` in float32, sqrt of a float32 expression, and the elementwise
+    normalisation in float32.  Statistics over the whole array, whatever its rank."""
+    v = np.asarray(vox, f32).copy()
+    nb = v.shape[0]
+    if filter_hot_pixel:
+        v[np.abs(v) > f32(20.0 / nb)] = 0
+    if mode == "maxmin":
+        return ((v - v.min()) / (v.max() - v.min() + f32(1e-8))).astype(f32)
+    if mode != "std":
+        return v
+    nz = v != 0
+    n = int(nz.sum())
+    if n == 0:
+        return v
+    nf = f32(n)
+    mean = f32(f32(v.astype(np.float64).sum()) / nf)
+    sq = f32(f32((v.astype(np.float64) ** 2).sum()) / nf)
+    std = np.sqrt(f32(sq - f32(mean * mean)), dtype=f32)
+    return (nz.astype(f32) * (v - mean) / f32(std + f32(1e-8))).astype(f32)
 
 
 class NoRandom:
@@ -105,21 +208,7 @@ class V2EOracle:
 
     def _lowpass(self, log_new, inten01, dt):
         """emulator_utils.py:49-101 (first-order, 0::2 pixels use qs)."""
-        if self.cutoff <= 0:
-            return log_new
-        if self.ql > 0:
-            tau0 = 1 / (math.pi * 2 * self.cutoff * self.ql)
-            eps = (inten01 * (f32(dt) / f32(tau0))).astype(f32)
-        else:
-            eps = np.ones_like(inten01)
-        if self.qs > 0:
-            tau1 = 1 / (math.pi * 2 * self.cutoff * self.qs)
-            eps1 = (inten01 * (f32(dt) / f32(tau1))).astype(f32)
-            eps[:, :, 0::2, 0::2] = eps1[:, :, 0::2, 0::2]
-        else:
-            eps[:, :, 0::2, 0::2] = 1
-        eps = np.minimum(eps, f32(1))
-        return ((f32(1) - eps) * self.lp + eps * log_new).astype(f32)
+        return low_pass_filter(log_new, self.lp, inten01, dt, self.cutoff, self.ql, self.qs)
 
     def forward(self, frames, t_frames):
         """frames (B, F, H, W) float32 intensities 0..255; t_frames (B, 2) or (B, F) seconds.
@@ -163,8 +252,8 @@ class V2EOracle:
             dt = f32(tf[n] - self.t_prev)
             if self.leak > 0:
                 rand = self.rng.randn((B, 1, H, W)).astype(f32)
-                leak = (f32(self.leak) * self.noise_rate * (f32(1) - f32(self.jitter) * rand)).astype(f32)
-                self.base = (self.base - dt * leak * self.pos_thres).astype(f32)
+                self.base = subtract_leak_current(self.base, self.leak, dt, self.pos_thres, self.jitter,
+                                                  self.noise_rate, rand)
             diff = (new - self.base).astype(f32)
             diff[~(np.abs(diff) > f32(1e-6))] = 0
             pol = np.sign(diff).astype(f32)
@@ -224,11 +313,4 @@ class V2EOracle:
 def preprocess_whole(vox):
     """event_preprocess_pytorch(mode='std', filter_hot_pixel=False) as v2e_model.py:526 calls it:
     statistics over the WHOLE (B, nb, H, W) tensor, float32 (utils/event_process.py:157-176)."""
-    v = vox.astype(f32)
-    nz = v != 0
-    n = int(nz.sum())
-    if n == 0:
-        return v
-    mean = f32(v.astype(np.float64).sum() / n)
-    std = f32(math.sqrt(max((v.astype(np.float64) ** 2).sum() / n - float(mean) ** 2, 0.0)))
-    return (nz.astype(f32) * (v - mean) / (std + f32(1e-8))).astype(f32)
+    return event_preprocess_pytorch(vox, mode="std", filter_hot_pixel=False)

@@ -93,8 +93,13 @@ def test_preprocess_thresholds_and_batch_shapes():
     got = ep.event_preprocess(raw, filter_hot_pixel=True).cpu().numpy()
     for b in range(3):
         assert_bits(got[b], fx.normalize_voxel(ref[b], True, "std", 25.0))
+    # the torch twin: threshold 20 / num_bins and float32 statistics (oracle pinned to the
+    # reference's own function by tests/test_oracle_v2e_golden.py)
+    from oracle import v2e_oracle as vo
+    from tests.conftest import rel_err
     got = ep.event_preprocess_pytorch(raw[1], filter_hot_pixel=True).cpu().numpy()
-    assert_bits(got, fx.normalize_voxel(ref[1], True, "std", 20.0))
+    want = vo.event_preprocess_pytorch(ref[1], "std", True)
+    assert rel_err(got, want) < 2e-6 and np.array_equal(got == 0, want == 0)
     assert torch.equal(raw.cpu(), torch.from_numpy(ref))      # not modified
 
 
@@ -139,3 +144,26 @@ def test_gpu_voxel_loader_matches_reference_path(tmp_path):
             off += int(sizes[s])
             ref = fx.normalize_voxel(fx.voxelize(win, 5, 32, 24), filter_hot_pixel=False)
             assert_bits(seq_events[s][b], ref)
+
+
+# ---- the reference's torch twins (utils/event_process.py:66-129, :157-176), pinned by
+# ---- vectors the reference functions themselves produced (tests/golden/make_golden_v2e.py)
+@pytest.mark.parametrize("tag,H,W", [("s", 48, 64), ("l", 180, 240)])
+def test_events_to_voxel_grid_pytorch_bit_exact(golden, tag, H, W):
+    d = golden("v2e_blocks.npz")
+    assert_bits(ep.events_to_voxel_grid_pytorch(d[f"tv_{tag}_events"], 5, W, H), d[f"tv_{tag}_vox"])
+
+
+def test_event_preprocess_pytorch_float32_statistics(golden):
+    """Bar 2e-6 of max|ref|: the float32 statistics round the sums once (ATen's own float32
+    reduction order is not restated); the zero mask is exact."""
+    from tests.conftest import rel_err
+    d = golden("v2e_blocks.npz")
+    whole = ep.event_preprocess_pytorch(torch.from_numpy(d["pp_whole_in"]).cuda(), mode="std",
+                                        filter_hot_pixel=False).cpu().numpy()     # v2e_model.py:526
+    assert rel_err(whole, d["pp_whole_out"]) < 2e-6
+    assert np.array_equal(whole == 0, d["pp_whole_out"] == 0)
+    grid = ep.event_preprocess_pytorch(torch.from_numpy(d["pp_grid_in"]).cuda(), mode="std",
+                                       filter_hot_pixel=True).cpu().numpy()
+    assert rel_err(grid, d["pp_grid_out"]) < 2e-6
+    assert np.array_equal(grid == 0, d["pp_grid_out"] == 0)

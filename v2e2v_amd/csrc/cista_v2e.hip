@@ -413,7 +413,8 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
         return CISTA_ERR_HIP;
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     // event_preprocess_pytorch(mode='std', filter_hot_pixel=False) over the whole tensor (:526)
-    return cista_voxel_preprocess(voxels, 1, B * nb, H, W, CISTA_VOXEL_STD, 0.0f, L.vox_ws, L.vox_ws_bytes, stream);
+    return cista_voxel_preprocess(voxels, 1, B * nb, H, W, CISTA_VOXEL_STD_F32, 0.0f, L.vox_ws, L.vox_ws_bytes,
+                                  stream);
 }
 
 }  // extern "C"

@@ -80,8 +80,28 @@ __device__ __forceinline__ bool event_value(const double *e, double first, doubl
     return true;
 }
 
+// events_to_voxel_grid_pytorch (:66-129) on a float64 events tensor: tis = floor(ts) must be
+// >= 0, the contributions are float32 (pols.float() * (1 - dts.float())), and index_add_ adds
+// them to the float32 grid in float32
+struct EvValT {
+    unsigned long long ti;
+    float vl, vr;
+};
+__device__ __forceinline__ bool event_value_torch(const double *e, double first, double dT, int nb, EvValT &o) {
+    const double ts = (double)(nb - 1) * (e[0] - first) / dT;        // :99
+    const double tis = floor(ts);                                      // :106
+    if (!(tis >= 0.0) || !(tis < 9.0e18)) return false;                // valid_indices &= tis >= 0
+    o.ti = (unsigned long long)tis;
+    const float dts = (float)(ts - tis);                               // :108, .float()
+    float pol = (float)e[3];
+    if (pol == 0.0f) pol = -1.0f;                                      // :104
+    o.vl = pol * (1.0f - dts);                                         // :109
+    o.vr = pol * dts;                                                  // :110
+    return true;
+}
+
 __global__ void vox_accum_kernel(const unsigned long long *keys, const int *vals, long long N, const double *ev,
-                                 const long long *off, int B, int nb, int H, int W, float *vox) {
+                                 const long long *off, int B, int nb, int H, int W, float *vox, int torch_acc) {
     const long long j = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (j >= N) return;
     const unsigned long long HW = (unsigned long long)H * W;
@@ -96,6 +116,19 @@ __global__ void vox_accum_kernel(const unsigned long long *keys, const int *vals
     float *out = vox + (size_t)b * nb * HW + p;
     long long end = j;
     while (end < N && keys[end] == key) ++end;
+    if (torch_acc) {                    // index_add_ #1 / #2 (:112-127), float32 adds
+        for (long long k = j; k < end; ++k) {
+            EvValT v;
+            if (event_value_torch(ev + 4 * (long long)vals[k], first, dT, nb, v) && v.ti < (unsigned long long)nb)
+                out[v.ti * HW] += v.vl;
+        }
+        for (long long k = j; k < end; ++k) {
+            EvValT v;
+            if (event_value_torch(ev + 4 * (long long)vals[k], first, dT, nb, v) && v.ti + 1 < (unsigned long long)nb)
+                out[(v.ti + 1) * HW] += v.vr;
+        }
+        return;
+    }
     // np.add.at #1 (:53-54): left contributions of the whole window, in event order
     for (long long k = j; k < end; ++k) {
         EvVal v;
@@ -246,7 +279,7 @@ __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox,
 }
 
 // one thread per window: numpy's chunk-sequential float32 accumulation, then float64 stats
-__global__ void vox_stats_kernel(const ChunkPart *parts, int nchunks, int B, WinStats *st) {
+__global__ void vox_stats_kernel(const ChunkPart *parts, int nchunks, int B, int mode, WinStats *st) {
     const int b = blockIdx.x * blockDim.x + threadIdx.x;
     if (b >= B) return;
     float s = 0.0f, q = 0.0f, mn = INFINITY, mx = -INFINITY;
@@ -262,7 +295,21 @@ __global__ void vox_stats_kernel(const ChunkPart *parts, int nchunks, int B, Win
     WinStats w;
     w.nnz = nnz; w.mn = mn; w.mx = mx;
     w.mean = 0.0; w.std = 0.0;
-    if (nnz > 0) {
+    if (nnz > 0 && mode == CISTA_VOXEL_STD_F32) {
+        // event_preprocess_pytorch (:168-175): float32 scalars throughout.  The sums are taken
+        // in float64 over the chunk partials and rounded once (ATen's float32 reduction order is
+        // not restated; the difference is the last bit of sum())
+        double sd = 0.0, qd = 0.0;
+        for (int c = 0; c < nchunks; ++c) {
+            sd += (double)parts[(size_t)b * nchunks + c].sum;
+            qd += (double)parts[(size_t)b * nchunks + c].sq;
+        }
+        const float nf = (float)nnz;
+        const float mean = (float)sd / nf;                   // sum() / num_nonzeros
+        const float var = (float)qd / nf - mean * mean;      // (v ** 2).sum() / n - mean ** 2
+        w.mean = mean;
+        w.std = sqrtf(var);
+    } else if (nnz > 0) {
         const double dn = (double)nnz;
         const double mean = (double)s / dn;                  // :148
         w.mean = mean;
@@ -282,6 +329,12 @@ __global__ void vox_apply_kernel(float *vox, long long n, int B, int mode, float
         if (w.nnz > 0) {                                     // :146
             const double mask = v != 0.0f ? 1.0 : 0.0;
             r = (float)(mask * ((double)v - w.mean) / (w.std + 1e-8));   // :152
+        }
+    } else if (mode == CISTA_VOXEL_STD_F32) {
+        const WinStats w = st[b];
+        if (w.nnz > 0) {                                     // :170, float32: mask * (v - mean) / (std + 1e-8)
+            const float mask = v != 0.0f ? 1.0f : 0.0f;
+            r = mask * (v - (float)w.mean) / ((float)w.std + 1e-8f);
         }
     } else if (mode == CISTA_VOXEL_MAXMIN) {
         const WinStats w = st[b];
@@ -346,7 +399,7 @@ int preprocess(float *voxels, int B, long long n, int mode, float thr, const Vox
         hipLaunchKernelGGL(vox_chunk_kernel, dim3(nchunks, B), dim3(MAX_LEAVES), 0, st, (const float *)voxels, n,
                            nchunks, thr, w.parts);
         hipLaunchKernelGGL(vox_stats_kernel, g1d(B, 64), dim3(64), 0, st, (const ChunkPart *)w.parts, nchunks, B,
-                           w.stats);
+                           mode, w.stats);
     }
     if (mode != CISTA_VOXEL_RAW || thr > 0.0f)
         hipLaunchKernelGGL(vox_apply_kernel, g1d(n * B), dim3(256), 0, st, voxels, n, B, mode, thr,
@@ -370,7 +423,9 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
                    size_t workspace_bytes, void *stream) {
     if (B < 0 || n_events < 0 || n_events > 0x7fffffffLL || num_bins <= 0 || height <= 0 || width <= 0)
         return CISTA_ERR_INVALID;
-    if (mode < CISTA_VOXEL_RAW || mode > CISTA_VOXEL_MAXMIN) return CISTA_ERR_INVALID;
+    const int torch_acc = (mode & CISTA_VOXEL_TORCH_ACCUM) != 0;
+    mode &= ~CISTA_VOXEL_TORCH_ACCUM;
+    if (mode < CISTA_VOXEL_RAW || mode > CISTA_VOXEL_STD_F32) return CISTA_ERR_INVALID;
     if (B == 0) return CISTA_OK;
     if (!offsets || !voxels || !workspace || (n_events > 0 && !events)) return CISTA_ERR_INVALID;
     const VoxWs w = carve(workspace, B, n_events, num_bins, height, width);
@@ -387,7 +442,8 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
                                                (const int *)w.v0, w.v1, (int)n_events, 0, bits, st) != hipSuccess)
             return CISTA_ERR_HIP;
         hipLaunchKernelGGL(vox_accum_kernel, g1d(n_events), dim3(256), 0, st, (const unsigned long long *)w.k1,
-                           (const int *)w.v1, n_events, events, offsets, B, num_bins, height, width, voxels);
+                           (const int *)w.v1, n_events, events, offsets, B, num_bins, height, width, voxels,
+                           torch_acc);
     }
     return preprocess(voxels, B, n, mode, hot_threshold, w, st);
 }
@@ -395,7 +451,7 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
 int cista_voxel_preprocess(float *voxels, int B, int num_bins, int height, int width, int mode,
                            float hot_threshold, void *workspace, size_t workspace_bytes, void *stream) {
     if (B < 0 || num_bins <= 0 || height <= 0 || width <= 0) return CISTA_ERR_INVALID;
-    if (mode < CISTA_VOXEL_RAW || mode > CISTA_VOXEL_MAXMIN) return CISTA_ERR_INVALID;
+    if (mode < CISTA_VOXEL_RAW || mode > CISTA_VOXEL_STD_F32) return CISTA_ERR_INVALID;
     if (B == 0) return CISTA_OK;
     if (!voxels || !workspace) return CISTA_ERR_INVALID;
     const VoxWs w = carve(workspace, B, 0, num_bins, height, width);

@@ -3,15 +3,19 @@
 Drop-in names:
 
 * ``events_to_voxel_grid(events, num_bins, width, height)``      <- utils/event_process.py:15-63
+* ``events_to_voxel_grid_pytorch(events, num_bins, width, height)`` <- utils/event_process.py:66-129
 * ``event_preprocess(voxel, mode='std', filter_hot_pixel=False)`` <- utils/event_process.py:132-154
 * ``event_preprocess_pytorch(voxel, mode, filter_hot_pixel=True)``<- utils/event_process.py:157-176
 * ``events_to_voxel_batch(windows, ...)``: many windows -> (B, num_bins, H, W) in one launch
   sequence (what the data readers need per sequence: data_readers/train_data_loaders.py:187-193,
   data_readers/video_readers.py:161-178).
 
-All of them run in libcista_hip.so (include/cista_voxel.h) and return CUDA tensors; the values
-are bit-identical to the reference's numpy path (voxel accumulation order, numpy's float32
-pairwise reduction for the 'std' statistics).  Differences from the reference, by design:
+All of them run in libcista_hip.so (include/cista_voxel.h) and return CUDA tensors.  The numpy
+twins are bit-identical to the reference's numpy path (voxel accumulation order, numpy's float32
+pairwise reduction for the 'std' statistics); the torch twins follow the reference's torch
+arithmetic: events_to_voxel_grid_pytorch bit-identically (float32 contributions, float32
+index_add_), event_preprocess_pytorch with float32 statistics (its sum() rounded once: ATen's
+reduction order may differ in the last bit, tests/test_gpu_voxel.py bounds it at 2e-6).  Differences from the reference, by design:
 inputs are never modified (the reference rewrites ``events[:, 0]``, the polarity column, and the
 voxel grid when filtering hot pixels), and events outside the grid are dropped instead of raising
 IndexError.  There is no CPU fallback: without the HIP library every call raises.
@@ -26,6 +30,8 @@ import torch
 from . import _lib
 
 MODES = {"none": 0, "raw": 0, "std": 1, "maxmin": 2}
+STD_F32 = 3                 # CISTA_VOXEL_STD_F32: event_preprocess_pytorch's float32 statistics
+TORCH_ACCUM = 0x10          # CISTA_VOXEL_TORCH_ACCUM: events_to_voxel_grid_pytorch accumulation
 _ws_cache: dict = {}
 
 
@@ -60,13 +66,15 @@ def _threshold(filter_hot_pixel: bool, num_bins: int, per_bin: float) -> float:
 
 def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode: str = "none",
                           filter_hot_pixel: bool = False, hot_threshold: float | None = None,
-                          out: torch.Tensor | None = None, device=None) -> torch.Tensor:
+                          out: torch.Tensor | None = None, device=None, torch_semantics: bool = False) -> torch.Tensor:
     """Voxelize (and optionally normalise) B event windows at once.
 
     ``windows`` is either a list of [N_b x 4] arrays/tensors (t, x, y, p), or a pair
     ``(events, offsets)`` with all windows concatenated (device tensors stay on the device).
     ``mode`` is 'none' (events_to_voxel_grid only), 'std' or 'maxmin' (event_preprocess);
     ``filter_hot_pixel`` uses the numpy threshold 25/num_bins unless ``hot_threshold`` is given.
+    ``torch_semantics``: the torch twins' arithmetic (events_to_voxel_grid_pytorch accumulation,
+    event_preprocess_pytorch float32 'std' statistics) instead of the numpy path's.
     Returns (B, num_bins, height, width) float32 on the GPU.
     """
     if num_bins <= 0 or width <= 0 or height <= 0:
@@ -88,12 +96,15 @@ def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode:
     elif out.shape != (B, num_bins, height, width) or out.dtype != torch.float32 or not out.is_contiguous():
         raise ValueError("out must be a contiguous float32 (B, num_bins, height, width) tensor")
     thr = hot_threshold if hot_threshold is not None else _threshold(filter_hot_pixel, num_bins, 25.0)
+    m = MODES[mode]
+    if torch_semantics:
+        m = (STD_F32 if m == MODES["std"] else m) | TORCH_ACCUM
     L = _lib.lib()
     nbytes = L.cista_voxel_workspace_bytes(B, N, num_bins, height, width)
     ws = _workspace(dev, nbytes)
     with torch.cuda.device(dev):
         _lib.check(L.cista_voxelize(_lib.ptr(events) if N else None, offsets.data_ptr(), B, N, num_bins, height,
-                                    width, MODES[mode], ctypes.c_float(thr), out.data_ptr(), ws.data_ptr(),
+                                    width, m, ctypes.c_float(thr), out.data_ptr(), ws.data_ptr(),
                                     ws.numel(), _lib.stream_handle(dev)), "cista_voxelize")
     return out
 
@@ -103,7 +114,13 @@ def events_to_voxel_grid(events, num_bins: int, width: int, height: int) -> torc
     return events_to_voxel_batch([events], num_bins, width, height)[0]
 
 
-def _preprocess(vox: torch.Tensor, mode: str, thr: float) -> torch.Tensor:
+def events_to_voxel_grid_pytorch(events, num_bins: int, width: int, height: int) -> torch.Tensor:
+    """Reference utils/event_process.py:66-129 on the GPU (a float64 events tensor's arithmetic):
+    (num_bins, height, width) float32."""
+    return events_to_voxel_batch([events], num_bins, width, height, torch_semantics=True)[0]
+
+
+def _preprocess(vox: torch.Tensor, mode: str, thr: float, f32_stats: bool = False) -> torch.Tensor:
     if not vox.is_cuda:
         raise _lib.CistaError("event_preprocess runs on a ROCm GPU only; move the voxel grid to cuda")
     squeeze = vox.dim() == 3
@@ -115,7 +132,8 @@ def _preprocess(vox: torch.Tensor, mode: str, thr: float) -> torch.Tensor:
     L = _lib.lib()
     ws = _workspace(res.device, L.cista_voxel_workspace_bytes(B, 0, nb, H, W))
     with torch.cuda.device(res.device):
-        _lib.check(L.cista_voxel_preprocess(res.data_ptr(), B, nb, H, W, MODES[mode], ctypes.c_float(thr),
+        m = STD_F32 if (f32_stats and mode == "std") else MODES[mode]
+        _lib.check(L.cista_voxel_preprocess(res.data_ptr(), B, nb, H, W, m, ctypes.c_float(thr),
                                             ws.data_ptr(), ws.numel(), _lib.stream_handle(res.device)),
                    "cista_voxel_preprocess")
     return res[0] if squeeze else res
@@ -128,6 +146,14 @@ def event_preprocess(event_voxel_grid: torch.Tensor, mode: str = "std", filter_h
 
 
 def event_preprocess_pytorch(event_voxel_grid: torch.Tensor, mode: str = "std", filter_hot_pixel: bool = True):
-    """Reference utils/event_process.py:157-176 (hot-pixel threshold 20/num_bins)."""
-    nb = event_voxel_grid.shape[-3]
-    return _preprocess(event_voxel_grid, mode, _threshold(filter_hot_pixel, nb, 20.0))
+    """Reference utils/event_process.py:157-176 (hot-pixel threshold 20/num_bins, float32
+    statistics).  Like the reference, the statistics span the WHOLE tensor it is given: a
+    (num_bins, H, W) grid, or a (B, num_bins, H, W) batch as v2e/v2e_model.py:526 passes it
+    (the threshold then uses the reference's shape[0])."""
+    nb = event_voxel_grid.shape[0]
+    v = event_voxel_grid
+    if v.dim() == 4:                    # one statistics window over the whole batch
+        B, n1, H, W = v.shape
+        return _preprocess(v.reshape(1, B * n1, H, W), mode, _threshold(filter_hot_pixel, nb, 20.0),
+                           f32_stats=True).reshape(B, n1, H, W)
+    return _preprocess(v, mode, _threshold(filter_hot_pixel, nb, 20.0), f32_stats=True)

@@ -34,6 +34,79 @@ class CistaV2EHostState(ctypes.Structure):
     _fields_ = [("initialized", ctypes.c_int), ("t_previous", ctypes.c_float), ("draw", ctypes.c_ulonglong)]
 
 
+class EventCount:
+    """The emulator's event count, kept on the device until it is read (the reference returns
+    a Python int, v2e_model.py:536; reading it per pack would be a host sync per pack).  Acts as
+    an int wherever one is used: int(), comparisons, arithmetic, formatting."""
+
+    __slots__ = ("_t", "_v")
+
+    def __init__(self, t):
+        self._t, self._v = t, None
+
+    def __int__(self):
+        if self._v is None:
+            self._v = int(self._t.item())
+            self._t = None
+        return self._v
+
+    __index__ = __int__
+
+    def __float__(self):
+        return float(int(self))
+
+    def __eq__(self, o):
+        return int(self) == o
+
+    def __ne__(self, o):
+        return int(self) != o
+
+    def __lt__(self, o):
+        return int(self) < o
+
+    def __le__(self, o):
+        return int(self) <= o
+
+    def __gt__(self, o):
+        return int(self) > o
+
+    def __ge__(self, o):
+        return int(self) >= o
+
+    def __hash__(self):
+        return hash(int(self))
+
+    def __add__(self, o):
+        return int(self) + o
+
+    __radd__ = __add__
+
+    def __mul__(self, o):
+        return int(self) * o
+
+    __rmul__ = __mul__
+
+    def __sub__(self, o):
+        return int(self) - o
+
+    def __rsub__(self, o):
+        return o - int(self)
+
+    def __truediv__(self, o):
+        return int(self) / o
+
+    def __bool__(self):
+        return int(self) != 0
+
+    def __repr__(self):
+        return repr(int(self))
+
+    __str__ = __repr__
+
+    def __format__(self, spec):
+        return format(int(self), spec)
+
+
 class EventEmulator(torch.nn.Module):
     """v2e_model.py:31-156 constructor surface."""
 
@@ -89,7 +162,8 @@ class EventEmulator(torch.nn.Module):
         if status == 1 and self.hs.initialized:
             raise ValueError("this frame time must be later than previous frame time")   # :339-342
         _lib.check(status, "cista_v2e_forward")
-        self.num_events = int(nev.item())
+        # no host sync per pack: the count stays a device scalar until someone reads it
+        self.num_events = EventCount(nev)
         return out, self.num_events
 
 
