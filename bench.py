@@ -33,24 +33,37 @@ import time
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-MACS_PER_FRAME_C64 = 22_793_011_200          # 180x240, C=64, depth 5, bins 5
 PEAK_F16_MFMA_TFLOPS = 2500.0                # MI355X dense fp16/bf16 MFMA (MI355X_MICROARCH.md)
 SPLIT_PASSES = 3
 PEAK_F32_MFMA_TFLOPS = 157.3                 # MI355X dense fp32 matrix (BASELINE.md framing)
 HBM_TBPS = 8.0                               # MI355X HBM3E
-BYTES_PER_FRAME = 34_387_200                 # 4*H*W*(num_bins + 2 + 3C): voxel, prev image, states in/out, frame
 
 
 def parse():
+    """Flags: the driver's (--gpus/--steps/--warmup) and the reference harness's names for the
+    model / data (utils/configs.py:6-91: --image_dim, -b/--num_bins, -d/--depth,
+    -c/--base_channels, -s/--len_sequence, --batch_size, --num_events, --num_pack_frames);
+    the older spellings stay as aliases."""
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--batch", type=int, default=64, help="sequences per GPU")
-    p.add_argument("--len-seq", type=int, default=15)
-    p.add_argument("--height", type=int, default=180)
-    p.add_argument("--width", type=int, default=240)
-    p.add_argument("--num-events", type=int, default=15000)
+    p.add_argument("--batch_size", "--batch", dest="batch", type=int, default=64, help="sequences per GPU")
+    p.add_argument("-s", "--len_sequence", "--len-seq", dest="len_seq", type=int, default=15)
+    p.add_argument("--image_dim", nargs=2, type=int, default=None, metavar=("H", "W"),
+                   help="frame height and width (default 180 240; v2e2v mode 720 1280)")
+    p.add_argument("--height", type=int, default=None)
+    p.add_argument("--width", type=int, default=None)
+    p.add_argument("-b", "--num_bins", type=int, default=5)
+    p.add_argument("-d", "--depth", type=int, default=5)
+    p.add_argument("-c", "--base_channels", type=int, default=64)
+    p.add_argument("--num_events", "--num-events", dest="num_events", type=int, default=15000)
+    p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
+                   help="timed region: the whole L-frame recurrence replayed as one hipGraph "
+                        "(v2e2v_amd/sequence.py) or the eager per-frame module calls; auto = both "
+                        "measured, the faster reported (the other in 'eager_vs_graph')")
+    p.add_argument("--sweep", default="1,8,32,64,128",
+                   help="batch sizes of the small-batch / latency sweep (empty: skip)")
     p.add_argument("--cpu-frames", type=int, default=15,
                    help="recurrent frames per CPU-baseline sequence (B=1); sequences repeat to ~10 s")
     p.add_argument("--no-cpu-baseline", action="store_true")
@@ -58,15 +71,19 @@ def parse():
     p.add_argument("--mode", choices=["infer", "train", "v2e2v"], default="infer",
                    help="infer: the headline metric (config c2); train: BPTT step (configs c3/c4); "
                         "v2e2v: emulator + reconstruction at 720x1280 (config c5)")
-    p.add_argument("--pack-frames", type=int, default=10, help="v2e2v: frames per reconstruction")
+    p.add_argument("--num_pack_frames", "--pack-frames", dest="pack_frames", type=int, default=10,
+                   help="v2e2v: frames per reconstruction")
     args = p.parse_args()
-    if args.mode == "train" and "--batch" not in sys.argv:
+    given = lambda *names: any(a in sys.argv for a in names)    # noqa: E731
+    if args.mode == "train" and not given("--batch", "--batch_size"):
         args.batch = 8            # BASELINE config c3: batch 8 per GPU (c4: 8 GPUs x 8 = 64)
-    if args.mode == "v2e2v":
-        if "--batch" not in sys.argv:
-            args.batch = 1        # config c5: one HFR video per GPU
-        if "--height" not in sys.argv:
-            args.height, args.width = 720, 1280
+    H, W = (180, 240) if args.mode != "v2e2v" else (720, 1280)
+    if args.image_dim:
+        H, W = args.image_dim
+    args.height = args.height or H
+    args.width = args.width or W
+    if args.mode == "v2e2v" and not given("--batch", "--batch_size"):
+        args.batch = 1            # config c5: one HFR video per GPU
     return args
 
 
@@ -78,9 +95,9 @@ def v2e2v_main(args, torch, vd, rank, world, device):
     import types
     from v2e2v_amd.v2e import V2E2VNet
     B, L, H, W, P = args.batch, args.len_seq, args.height, args.width, args.pack_frames
-    cfgs = types.SimpleNamespace(event_mode="voxel_grid", num_bins=5, pl=1.0, ps=1.0, ql=1.0, qs=1.0, C=0.2,
-                                 threshold_sigma=0.03, cutoff_hz=30.0, refractory_period_s=0.001,
-                                 base_channels=64, depth=5)
+    cfgs = types.SimpleNamespace(event_mode="voxel_grid", num_bins=args.num_bins, pl=1.0, ps=1.0, ql=1.0, qs=1.0,
+                                 C=0.2, threshold_sigma=0.03, cutoff_hz=30.0, refractory_period_s=0.001,
+                                 base_channels=args.base_channels, depth=args.depth)
     net = V2E2VNet(cfgs, [H, W], device)
     he_init_(torch, net.e2v_net, seed=7)
     net = net.to(device).eval()
@@ -149,7 +166,8 @@ def train_main(args, torch, vd, rank, world, device):
     from v2e2v_amd.losses import SSIM
     ssim_fn = SSIM(data_range=1, size_average=True, channel=1, nonnegative_ssim=False)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
-    model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
+    nb, C, depth = args.num_bins, args.base_channels, args.depth
+    model = CistaLSTCNet([H, W], base_channels=C, depth=depth, num_bins=nb)
     he_init_(torch, model, seed=7)
     model = model.to(device).train()
     net = model
@@ -157,7 +175,7 @@ def train_main(args, torch, vd, rank, world, device):
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index],
                                                         broadcast_buffers=False)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
-    vox = synth_voxels(torch, L, B, 5, H, W, args.num_events, seed=2000 + rank, device=device)
+    vox = synth_voxels(torch, L, B, nb, H, W, args.num_events, seed=2000 + rank, device=device)
     target = torch.rand(B, 1, H, W, device=device, generator=torch.Generator(device=device).manual_seed(3))
 
     def step():
@@ -183,6 +201,19 @@ def train_main(args, torch, vd, rank, world, device):
     vd.barrier()
     elapsed = vd.max_over_ranks(time.perf_counter() - t0, device)
     frames = world * B * L * args.steps
+    from v2e2v_amd import _lib
+    macs_frame, _ = frame_work(_lib, model, H, W)
+    # a BPTT frame costs the forward plus dgrad and wgrad of every conv: 3x the forward FLOPs
+    # (SURVEY 8(d) "training FLOPs ~ 3x fwd"), run on the same split-f16 MFMA peak
+    train_tf = frames / elapsed / world * 3 * 2 * macs_frame / 1e12
+    peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
+    roofline = dict(bound="mfma", achieved=round(train_tf, 2), peak=round(peak, 1), unit="TFLOP/s",
+                    frac=round(train_tf / peak, 4), traffic=None, kernel="whole BPTT step (per GPU)",
+                    note="achieved = 3 x forward algorithmic FLOPs per frame x frames/s per GPU; "
+                         "peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = train_cpu_baseline(torch, model, vox, target, L, H, W)
     if rank == 0:
         print(json.dumps({
             "metric": "BPTT training frames/sec at 180x240 5-bin depth=5 (len_sequence 15)",
@@ -195,9 +226,33 @@ def train_main(args, torch, vd, rank, world, device):
                        "batch_per_gpu": B, "global_batch": B * world, "len_sequence": L,
                        "parallelism": f"ddp{world}" if world > 1 else "single"},
             "loss": float(loss.item()),
+            "roofline": roofline, "cpu_baseline": cpu,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def train_cpu_baseline(torch, model, vox, target, L, H, W, min_s=10.0, max_steps=4):
+    """The training step's CPU baseline: the PyTorch-CPU restatement (oracle/cista_oracle_torch.py,
+    pinned to the golden vectors) under autograd -- train_e2v.py:108-130 semantics, B=1, the
+    same L frames and size -- on this host's cores, repeated to ~10 s."""
+    from oracle import fixtures as fx
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU, bptt_step
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(cores)
+    sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
+    net = CistaLSTCTorchCPU(fx.collapse_tied(sd, model.depth), model.depth, requires_grad=True)
+    v = vox[:, :1].cpu().numpy()
+    tg = target[:1].cpu().numpy()
+    steps, dt = 0, 0.0
+    while steps < max_steps and (dt < min_s or steps == 0):
+        t0 = time.perf_counter()
+        bptt_step(net, v, tg)
+        dt += time.perf_counter() - t0
+        steps += 1
+    return dict(value=steps * L / dt, unit="frames/s", cores=int(cores), kind="port",
+                sample=f"{steps} BPTT step(s) of {L} frames at {H}x{W}, B=1 (L1 on the last frame, "
+                       f"autograd through the PyTorch-CPU restatement), {cores} threads, {dt:.1f} s")
 
 
 # ------------------------------------------------------------------ synthetic inputs (GPU)
@@ -386,11 +441,64 @@ def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
                        f"{cores} threads, {dt:.1f} s"), ps, rel
 
 
+def frame_work(lib_mod, model, H, W):
+    """Algorithmic work of one frame (B = 1) of this model config: MACs summed over the frame's
+    layers (the library's cista_layer_macs, SURVEY 2.3 closed form; 22 793 011 200 at 180x240,
+    C=64, depth 5, 5 bins) and HBM bytes 4*H*W*(num_bins + 2 + 3C) (voxel, prev
+    image, states in and out, frame)."""
+    L = lib_mod.lib()
+    cfg = model._cfg()
+    macs = 0.0
+    for lid, name in enumerate(lib_mod.LAYERS):
+        macs += L.cista_layer_macs(ctypes.byref(cfg), lid, 1, H, W) * (model.depth if name.startswith("ista") else 1)
+    return macs, 4 * H * W * (model.num_bins + 2 + 3 * model.base_channels)
+
+
+def time_steps(torch, fn, steps, warmup, vd=None, device=None):
+    """Seconds for `steps` calls of fn after `warmup`, bracketed by barrier + synchronize."""
+    for _ in range(warmup):
+        out = fn()
+    torch.cuda.synchronize()
+    if vd is not None:
+        vd.barrier()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        out = fn()
+    torch.cuda.synchronize()
+    if vd is not None:
+        vd.barrier()
+    return time.perf_counter() - t0, out
+
+
+def batch_sweep(torch, model, args, device, batches):
+    """Small-batch / latency sweep (B in {1, 8, 32, 64, 128}): per batch size the
+    per-frame latency (one recurrent frame of B sequences) and frames/s, eager per-frame module
+    calls and the whole-sequence hipGraph replay; rank 0 only, a few sequences each."""
+    from v2e2v_amd.sequence import CistaSequence
+    H, W, L = args.height, args.width, args.len_seq
+    out = {}
+    for B in batches:
+        vox = synth_voxels(torch, L, B, model.num_bins, H, W, args.num_events, seed=5000 + B, device=device)
+        steps = 8 if B <= 8 else 3
+        with torch.no_grad():
+            te, _ = time_steps(torch, lambda: run_sequence(torch, model, vox, B, H, W, device), steps, 1)
+            seq = CistaSequence(model, vox)
+            tg, _ = time_steps(torch, seq.run, steps, 1)
+            seq.close()
+        out[str(B)] = {"frame_ms_eager": round(te / (steps * L) * 1e3, 4),
+                       "frame_ms_graph": round(tg / (steps * L) * 1e3, 4),
+                       "frames_per_s_eager": round(B * L * steps / te, 1),
+                       "frames_per_s_graph": round(B * L * steps / tg, 1)}
+        del vox
+    return out
+
+
 def main():
     args = parse()
     import torch
     from v2e2v_amd import CistaLSTCNet, _lib
     from v2e2v_amd import dist as vd
+    from v2e2v_amd.sequence import CistaSequence
 
     rank, world, local_rank = vd.env_rank()
     device = torch.device("cuda", local_rank)
@@ -401,27 +509,33 @@ def main():
     if args.mode == "v2e2v":
         return v2e2v_main(args, torch, vd, rank, world, device)
     B, L, H, W = args.batch, args.len_seq, args.height, args.width
+    nb, C, depth = args.num_bins, args.base_channels, args.depth
 
-    model = CistaLSTCNet([H, W], base_channels=64, depth=5, num_bins=5)
+    model = CistaLSTCNet([H, W], base_channels=C, depth=depth, num_bins=nb)
     he_init_(torch, model, seed=7)
     model = model.to(device).eval()
+    macs_frame, bytes_frame = frame_work(_lib, model, H, W)
     # sequences of this rank: a disjoint shard (seed offset by rank)
-    vox = synth_voxels(torch, L, B, 5, H, W, args.num_events, seed=1000 + rank, device=device)
+    vox = synth_voxels(torch, L, B, nb, H, W, args.num_events, seed=1000 + rank, device=device)
     torch.cuda.synchronize()
 
+    # timed region: K steps of the L-frame recurrence over resident voxels, either as eager
+    # per-frame module calls (the reference harness's loop) or as one hipGraph replay per step
+    timings = {}
     with torch.no_grad():
-        for _ in range(args.warmup):
-            run_sequence(torch, model, vox, B, H, W, device)
-        torch.cuda.synchronize()
-        vd.barrier()
-        t0 = time.perf_counter()
-        for _ in range(args.steps):
-            rec, _ = run_sequence(torch, model, vox, B, H, W, device)
-        torch.cuda.synchronize()
-        vd.barrier()
-        elapsed = time.perf_counter() - t0
+        if args.graph in ("auto", "off"):
+            timings["eager"] = time_steps(torch, lambda: run_sequence(torch, model, vox, B, H, W, device),
+                                          args.steps, args.warmup, vd, device)
+        if args.graph in ("auto", "on"):
+            seq = CistaSequence(model, vox)
+            timings["graph"] = time_steps(torch, lambda: seq.run()[0][-1], args.steps, args.warmup, vd, device)
+    # the same choice on every rank: the max over ranks of each path, then the faster path
+    el = {k: vd.max_over_ranks(v[0], device) for k, v in timings.items()}
+    path = min(el, key=el.get)
+    elapsed = el[path]
+    rec = timings[path][1]
+    rec = rec[0] if isinstance(rec, tuple) else rec
     finite = bool(torch.isfinite(rec).all())
-    elapsed = vd.max_over_ranks(elapsed, device)
     frames = world * B * L * args.steps
     value = frames / elapsed
 
@@ -449,7 +563,7 @@ def main():
         except (OSError, ValueError, KeyError):
             pass
 
-    voxelizer = (time_voxelizer(torch, B * L, args.num_events, 5, H, W, device, cpu_leg=not args.no_cpu_baseline)
+    voxelizer = (time_voxelizer(torch, B * L, args.num_events, nb, H, W, device, cpu_leg=not args.no_cpu_baseline)
                  if rank == 0 else None)
 
     cpu = None
@@ -460,8 +574,14 @@ def main():
 
     if rank == 0:
         frame_ms = sum(v["ms"] * v["launches_per_frame"] for v in layers.values())
+        sweep = None
+        if args.sweep:
+            sweep = batch_sweep(torch, model, args, device, [int(x) for x in args.sweep.split(",") if x])
+        cfg_name = f"{H}x{W} {nb}-bin depth={depth} C={C}"
         out = {
-            "metric": "reconstructed frames/sec/GPU at 180x240 5-bin depth=5; PSNR vs ref",
+            "metric": "reconstructed frames/sec/GPU at 180x240 5-bin depth=5; PSNR vs ref"
+                      if (H, W, nb, depth, C) == (180, 240, 5, 5, 64)
+                      else f"reconstructed frames/sec/GPU at {cfg_name}; PSNR vs ref",
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
@@ -473,22 +593,25 @@ def main():
             "vs_baseline": None,
             "dtype": "f32",
             "data": "synthetic (GPU-generated 15000-event voxels; He-scaled random-init weights)",
-            "config": {"workload": f"CISTA-LSTC inference {H}x{W} 5-bin depth=5 C=64, "
+            "config": {"workload": f"CISTA-LSTC inference {cfg_name}, "
                                    f"len_sequence={L}, {B} sequences/GPU",
+                       "timed_path": "whole-sequence hipGraph replay (v2e2v_amd/sequence.py)"
+                                     if path == "graph" else "eager per-frame CistaLSTCNet.forward",
                        "batch_per_gpu": B, "len_sequence": L, "height": H, "width": W,
                        "num_events": args.num_events, "parallelism": f"replicas x{world}",
                        "precision": "split3-f16 MFMA (fp32 accumulate)"},
             "frames_per_s_per_gpu": round(value / world, 2),
-            "tflops_effective": round(value * 2 * MACS_PER_FRAME_C64 / 1e12, 2),
+            "tflops_effective": round(value * 2 * macs_frame / 1e12, 2),
+            "eager_vs_graph_frames_per_s": {k: round(frames / v, 1) for k, v in el.items()},
             # whole-path fractions of BASELINE.md's roofline framing, per GPU: algorithmic FLOPs
             # and bytes per frame x frames/s over the peak
             "path_fractions": {
-                "mfma_frac_vs_split3_peak": round(value / world * 2 * MACS_PER_FRAME_C64
+                "mfma_frac_vs_split3_peak": round(value / world * 2 * macs_frame
                                                   / (PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES * 1e12), 4),
-                "mfma_frac_vs_fp32_matrix_peak": round(value / world * 2 * MACS_PER_FRAME_C64
+                "mfma_frac_vs_fp32_matrix_peak": round(value / world * 2 * macs_frame
                                                        / (PEAK_F32_MFMA_TFLOPS * 1e12), 4),
-                "hbm_frac": round(value / world * BYTES_PER_FRAME / (HBM_TBPS * 1e12), 5),
-                "hbm_gbps_algorithmic": round(value / world * BYTES_PER_FRAME / 1e9, 1)},
+                "hbm_frac": round(value / world * bytes_frame / (HBM_TBPS * 1e12), 5),
+                "hbm_gbps_algorithmic": round(value / world * bytes_frame / 1e9, 1)},
             "psnr_vs_ref": None if psnr_vs_ref is None else round(psnr_vs_ref, 2),
             "max_rel_err_vs_ref": rel_vs_ref,
             "outputs_finite": finite,
@@ -498,6 +621,7 @@ def main():
             "layers_tflops": {k: round(v["tflops"], 1) for k, v in layers.items()},
             "sum_of_kernels_ms_per_frame_batch": round(frame_ms, 3),
             "voxelizer": voxelizer,
+            "batch_sweep": sweep,
         }
         print(json.dumps(out), flush=True)
     if world > 1:

@@ -119,6 +119,21 @@ int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int
                   const cista_frame_io *io, void *workspace, size_t workspace_bytes,
                   void *stream);
 
+/* ---- HIP graphs (no reference counterpart: a launch-overhead optimisation) ----
+ * cista_sequence_capture records `n_frames` consecutive cista_forward frames -- ~21 kernel
+ * launches each -- into ONE hipGraph (captured on a private stream, so any caller stream can
+ * replay it).  Frame f reads io[f] and must have the buffers cista_forward would; the recurrent
+ * chaining is the caller's choice of pointers (io[f+1]'s prev pointers = io[f]'s outputs).
+ * Every pointer is baked into the graph: replays recompute on whatever those buffers hold.
+ * The parameters must be packed (and stay packed) before capture.  cista_sequence_launch
+ * enqueues one replay on `stream`; cista_sequence_destroy frees the graph. */
+typedef struct cista_sequence cista_sequence;
+int  cista_sequence_capture(const cista_config *cfg, const void *packed, int B, int H, int W,
+                            const cista_frame_io *io, int n_frames, void *workspace,
+                            size_t workspace_bytes, cista_sequence **out);
+int  cista_sequence_launch(cista_sequence *seq, void *stream);
+void cista_sequence_destroy(cista_sequence *seq);
+
 /* ---- stage entries (the reference module boundaries; used by parity tests) ---- */
 /* x1 (B,h,w,C) NHWC = W0(cat(We(events), Wi(prev_image)))                              */
 int cista_stage_input(const cista_config *cfg, const void *packed, int B, int H, int W,

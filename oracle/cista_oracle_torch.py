@@ -21,8 +21,9 @@ import torch.nn.functional as F
 class CistaLSTCTorchCPU:
     """CistaLSTCNet.forward (reference e2v/e2v_model.py:41-90) as ATen CPU calls."""
 
-    def __init__(self, params: dict, depth: int = 5, dtype=torch.float32):
-        self.p = {k: torch.as_tensor(np.asarray(v)).to(dtype) for k, v in params.items()}
+    def __init__(self, params: dict, depth: int = 5, dtype=torch.float32, requires_grad: bool = False):
+        self.p = {k: torch.as_tensor(np.asarray(v)).to(dtype).requires_grad_(requires_grad)
+                  for k, v in params.items()}
         self.depth = depth
         self.dtype = dtype
         self.C = self.p["W0.conv2d.weight"].shape[0]
@@ -59,8 +60,12 @@ class CistaLSTCTorchCPU:
         c = torch.sigmoid(gr) * c_prev + torch.sigmoid(gi) * torch.tanh(gc)  # :119-127
         return torch.sigmoid(go) * torch.tanh(c), c                          # :128
 
-    @torch.no_grad()
     def forward(self, events, prev_image, prev_states=None):
+        with torch.no_grad():
+            return self.forward_grad(events, prev_image, prev_states)
+
+    def forward_grad(self, events, prev_image, prev_states=None):
+        """The same forward under autograd (the CPU baseline of the BPTT training step)."""
         if prev_states is None:                                              # e2v_model.py:57-58
             prev_states = [None, None, None]
         x_e = self._conv("We.conv2d", events)                                # :62
@@ -93,3 +98,21 @@ class CistaLSTCTorchCPU:
             recs.append(prev)
         st = [states[0].numpy(), states[1].numpy(), (states[2][0].numpy(), states[2][1].numpy())]
         return torch.stack(recs).numpy(), st
+
+
+def bptt_step(net: CistaLSTCTorchCPU, voxels, target):
+    """One train_e2v.py:108-130 step on the CPU restatement (bench.py's training cpu_baseline):
+    L recurrent frames, prev_img = output.clone() (not detached), L1 on the last frame, one
+    backward through the whole sequence; returns the loss."""
+    v = torch.as_tensor(np.asarray(voxels)).to(net.dtype)
+    F_, B, _, H, W = v.shape
+    prev = torch.zeros(B, 1, H, W, dtype=net.dtype)
+    states = None
+    for f in range(F_):
+        out, states = net.forward_grad(v[f], prev, states)
+        prev = out.clone()
+    loss = torch.nn.functional.l1_loss(out, torch.as_tensor(np.asarray(target)).to(net.dtype))
+    for t in net.p.values():
+        t.grad = None
+    loss.backward()
+    return float(loss.item())

@@ -1,0 +1,57 @@
+"""Whole-sequence hipGraph replay (v2e2v_amd/sequence.py, include/cista_lstc.h cista_sequence_*):
+the graph replays exactly the kernels the eager module launches, so its frames and states must
+be BIT-identical to the per-frame CistaLSTCNet loop of the reference harness
+(test_e2v.py:105-117: prev_image = previous output, states carried)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import fixtures as fx
+from v2e2v_amd import CistaLSTCNet
+from v2e2v_amd.sequence import CistaSequence
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def model(H, W, seed=7):
+    m = CistaLSTCNet([H, W])
+    p = fx.stress_params(64, 5, 5, seed=seed)
+    m.load_state_dict(fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in p.items()}, 5))
+    return m.to(DEV).eval()
+
+
+def eager(m, vox, prev, states):
+    recs = []
+    with torch.no_grad():
+        for f in range(vox.shape[0]):
+            prev, states = m(vox[f], prev, states)
+            recs.append(prev)
+    return torch.stack(recs), states
+
+
+@pytest.mark.parametrize("B,H,W,L", [(1, 180, 240, 4), (3, 64, 96, 5)])
+def test_graph_replay_bit_identical_to_eager(B, H, W, L):
+    m = model(H, W)
+    vox = torch.from_numpy(fx.synthetic_voxels(L, B, 5, H, W, n_events=fx.density_matched_events(H, W), seed=3)).to(DEV)
+    seq = CistaSequence(m, vox)
+    for _ in range(2):                                   # replays are repeatable
+        recs, st = seq.run()
+        torch.cuda.synchronize()
+        ref, rst = eager(m, vox, torch.zeros(B, 1, H, W, device=DEV), None)
+        assert torch.equal(recs, ref)
+        for a, b in zip([st[0], st[1], st[2][0], st[2][1]], [rst[0], rst[1], rst[2][0], rst[2][1]]):
+            assert torch.equal(a, b)
+    # next sequence: new voxels in place, continuing from the last states and frame
+    prev, states = recs[-1].clone(), [st[0].clone(), st[1].clone(), (st[2][0].clone(), st[2][1].clone())]
+    seq2 = CistaSequence(m, vox, prev_image=prev, prev_states=states)
+    vox.mul_(-0.5)
+    r2 = seq2.run()[0].clone()           # run() returns its own (reused) buffers
+    ref2, _ = eager(m, vox, prev, states)
+    assert torch.equal(r2, ref2)
+    # a parameter update is picked up (re-pack + re-capture)
+    with torch.no_grad():
+        m.final_conv.conv2d.bias.add_(0.25)
+    r3, _ = seq2.run()
+    ref3, _ = eager(m, vox, prev, states)
+    assert torch.equal(r3, ref3) and not torch.equal(r3, r2)

@@ -100,6 +100,10 @@ def _declare(lib):
                                    P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
+        "cista_sequence_capture": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO), c_int,
+                                           c_void_p, c_size_t, P(c_void_p)]),
+        "cista_sequence_launch": (c_int, [c_void_p, c_void_p]),
+        "cista_sequence_destroy": (None, [c_void_p]),
         # include/cista_voxel.h
         "cista_voxel_workspace_bytes": (c_size_t, [c_int, ctypes.c_longlong, c_int, c_int, c_int]),
         "cista_voxelize": (c_int, [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_int, c_int, c_int,

@@ -1125,6 +1125,53 @@ int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int
     return run_layers(f, tail, 4);
 }
 
+struct cista_sequence {
+    hipGraph_t graph;
+    hipGraphExec_t exec;
+};
+
+int cista_sequence_capture(const cista_config *cfg, const void *packed, int B, int H, int W,
+                           const cista_frame_io *io, int n_frames, void *workspace, size_t workspace_bytes,
+                           cista_sequence **out) {
+    if (!out || !io || n_frames <= 0) return CISTA_ERR_INVALID;
+    *out = nullptr;
+    hipStream_t cs;
+    if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return CISTA_ERR_HIP;
+    // a first eager frame on the private stream: one-time kernel attributes (LDS limits) are set
+    // outside the capture, and argument errors surface before any graph exists
+    int status = cista_forward(cfg, packed, B, H, W, &io[0], workspace, workspace_bytes, cs);
+    if (status == CISTA_OK && hipStreamSynchronize(cs) != hipSuccess) status = CISTA_ERR_HIP;
+    hipGraph_t g = nullptr;
+    if (status == CISTA_OK) {
+        if (hipStreamBeginCapture(cs, hipStreamCaptureModeThreadLocal) != hipSuccess) status = CISTA_ERR_HIP;
+        for (int f = 0; status == CISTA_OK && f < n_frames; ++f)
+            status = cista_forward(cfg, packed, B, H, W, &io[f], workspace, workspace_bytes, cs);
+        const hipError_t e = hipStreamEndCapture(cs, &g);   // always end a begun capture
+        if (status == CISTA_OK && e != hipSuccess) status = CISTA_ERR_HIP;
+    }
+    hipGraphExec_t ex = nullptr;
+    if (status == CISTA_OK && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) status = CISTA_ERR_HIP;
+    (void)hipStreamDestroy(cs);
+    if (status != CISTA_OK) {
+        if (g) (void)hipGraphDestroy(g);
+        return status;
+    }
+    *out = new cista_sequence{g, ex};
+    return CISTA_OK;
+}
+
+int cista_sequence_launch(cista_sequence *seq, void *stream) {
+    if (!seq) return CISTA_ERR_INVALID;
+    return hipGraphLaunch(seq->exec, static_cast<hipStream_t>(stream)) == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+}
+
+void cista_sequence_destroy(cista_sequence *seq) {
+    if (!seq) return;
+    (void)hipGraphExecDestroy(seq->exec);
+    (void)hipGraphDestroy(seq->graph);
+    delete seq;
+}
+
 int cista_stage_input(const cista_config *cfg, const void *packed, int B, int H, int W,
                       const float *events, const float *prev_image, float *x1, void *workspace,
                       size_t workspace_bytes, void *stream) {

@@ -118,9 +118,10 @@ __device__ __forceinline__ float relu_(float x) { return x != x ? x : fmaxf(x, 0
 // reference softshrink formula, base_layers.py:11-12: relu(x - l) - relu(-x - l)
 __device__ __forceinline__ float softshrink_(float x, float l) { return relu_(x - l) - relu_(-x - l); }
 
-// split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25); amax
-// tracks the largest staged magnitude: >= 65504 does not fit the fp16 hi part (range flag)
-__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, float &amax) {
+// split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25); hmax
+// keeps the running packed max of |hi|: it reaches inf exactly when a staged |x| >= 65520
+// does not fit the fp16 hi part (the range flag; 4 packed v_pk_max_f16 per 8 values)
+__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, f16x8 &hmax) {
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     f16x8 h, l;
 #pragma unroll
@@ -128,8 +129,8 @@ __device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &
         const _Float16 hb = (_Float16)v[i];
         h[i] = hb;
         l[i] = (_Float16)(v[i] - (float)hb);
-        amax = fmaxf(amax, fabsf(v[i]));
     }
+    hmax = __builtin_elementwise_max(hmax, __builtin_elementwise_abs(h));
     hi = __builtin_bit_cast(u32x4, h);
     lo = __builtin_bit_cast(u32x4, l);
 }
@@ -207,7 +208,7 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
 template <int STAGE>
 __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
                                             int ix0, int HH, int HWd, int HPpad,
-                                            const float *seg, int segC, int choff, float &amax) {
+                                            const float *seg, int segC, int choff, f16x8 &amax) {
     constexpr int BATCH = STAGE == STAGE_UP ? 2 : 4;
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
@@ -258,7 +259,7 @@ __device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, i
 template <int NI>
 __device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4 (&v0)[NI],
                                              const float4 (&v1)[NI], const int (&hps)[NI],
-                                             const int (&gs)[NI], float &amax) {
+                                             const int (&gs)[NI], f16x8 &amax) {
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         if (hps[u] < 0) continue;
@@ -422,7 +423,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    float amax = 0.0f;   // largest staged |x| of this thread (range flag, see ConvArgs.rflag)
+    f16x8 amax = {};     // running max of the staged |hi| parts (range flag, see ConvArgs.rflag)
     const int NT = a.N >> 4;
     const int nt0 = (nblk * WN + wn) * NW;
     const int kc0 = a.c0 >> 5;
@@ -553,7 +554,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     }
 
     // an activation beyond the fp16 range of the hi part (or inf): the result is not fp32-faithful
-    if (amax >= 65504.0f && a.rflag) *a.rflag = 1;
+    if (a.rflag) {
+        _Float16 m = amax[0];
+#pragma unroll
+        for (int i = 1; i < 8; ++i) m = m > amax[i] ? m : amax[i];
+        if (__builtin_isinf((float)m)) *a.rflag = 1;
+    }
 
     // ---------------------------------- epilogue ----------------------------------------
     // acc[m][n][j]: pixel row (wm*MT_W+m)*16 + 4*(lane>>4) + j, packed column (nt0+n)*16 + lane&15
