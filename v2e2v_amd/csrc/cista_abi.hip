@@ -232,9 +232,23 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #ifndef CISTA_S2DB
 #define CISTA_S2DB 0      // stride-2 W0: 0 single-buffered 128-px tiles; 1/2 double-buffered 64-px
 #endif
+#ifndef CISTA_SMALL_GRID
+#define CISTA_SMALL_GRID 1   // latency tiles for grids that would not fill the chip (small B)
+#endif
 #ifndef CISTA_WIDE
 #define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
 #endif
+// fewer than ~1.5 workgroups per CU with the throughput configuration (px x cols per WG)
+inline bool small_grid(const ConvArgs &a, int wg_px, int wg_cols) {
+#if CISTA_SMALL_GRID
+    const long px = (long)a.B * a.Hout * a.Wout;
+    return ((px + wg_px - 1) / wg_px) * ((a.N + wg_cols - 1) / wg_cols) < 384;
+#else
+    (void)a; (void)wg_px; (void)wg_cols;
+    return false;
+#endif
+}
+
 template <int STAGE, int EPI, int G>
 int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
@@ -255,6 +269,16 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
     } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2)) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
         constexpr bool FWD = STAGE == STAGE_S1;
+        if constexpr (FWD) {
+            // small batches (B = 1 is the reference harness's case): the throughput tiles below
+            // leave most CUs idle, so 64-pixel x 64-column workgroups trade MFMA efficiency
+            // for 3-6x more of them (latency per frame)
+            const int big_px = a.N % 256 == 0 ? 96 : 192, big_cols = a.N % 256 == 0 ? 256 : a.N % 128 == 0 ? 128 : 64;
+            if (a.N % 64 == 0 && small_grid(a, big_px, big_cols)) {
+                if constexpr (G == 4) return launch_conv_cfg<1, 4, 4, 1, STAGE, EPI, G, true, 2>(a, st);
+                else return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
+            }
+        }
         if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
             if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
         if constexpr (G == 4) {

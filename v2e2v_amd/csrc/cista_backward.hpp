@@ -149,7 +149,7 @@ __device__ __forceinline__ float wg_load_x(const WgradArgs &a, int b, int iy, in
         const float *base = seg + (size_t)b * a.Hin * a.Win * segC + cc;
         const float v00 = base[((size_t)y0 * a.Win + x0) * segC], v01 = base[((size_t)y0 * a.Win + x1) * segC];
         const float v10 = base[((size_t)y1 * a.Win + x0) * segC], v11 = base[((size_t)y1 * a.Win + x1) * segC];
-        return ly0 * (lx0 * v00 + lx1 * v01) + ly1 * (lx0 * v10 + lx1 * v11);
+        return bilerp(ly0, ly1, lx0, lx1, v00, v01, v10, v11);
     } else if constexpr (XS == XS_NCHW) {
         const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
         return seg[(((size_t)b * segC + cc) * a.Hin + y) * a.Win + x];
@@ -183,10 +183,10 @@ __device__ __forceinline__ float4 wg_load_x4(const WgradArgs &a, int b, int iy, 
         const float4 v10 = *reinterpret_cast<const float4 *>(base + ((size_t)y1 * a.Win + x0) * segC);
         const float4 v11 = *reinterpret_cast<const float4 *>(base + ((size_t)y1 * a.Win + x1) * segC);
         float4 r;
-        r.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
-        r.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
-        r.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
-        r.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+        r.x = bilerp(ly0, ly1, lx0, lx1, v00.x, v01.x, v10.x, v11.x);
+        r.y = bilerp(ly0, ly1, lx0, lx1, v00.y, v01.y, v10.y, v11.y);
+        r.z = bilerp(ly0, ly1, lx0, lx1, v00.z, v01.z, v10.z, v11.z);
+        r.w = bilerp(ly0, ly1, lx0, lx1, v00.w, v01.w, v10.w, v11.w);
         return r;
     } else {
         if constexpr (XS == XS_NCHW)   // never selected on the host (vec4 = 0); plain loads
@@ -700,10 +700,10 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const float *x, float *
     const float4 v10 = *(const float4 *)(base + ((size_t)y1 * w + x0) * C);
     const float4 v11 = *(const float4 *)(base + ((size_t)y1 * w + x1) * C);
     float4 r;
-    r.x = ly0 * (lx0 * v00.x + lx1 * v01.x) + ly1 * (lx0 * v10.x + lx1 * v11.x);
-    r.y = ly0 * (lx0 * v00.y + lx1 * v01.y) + ly1 * (lx0 * v10.y + lx1 * v11.y);
-    r.z = ly0 * (lx0 * v00.z + lx1 * v01.z) + ly1 * (lx0 * v10.z + lx1 * v11.z);
-    r.w = ly0 * (lx0 * v00.w + lx1 * v01.w) + ly1 * (lx0 * v10.w + lx1 * v11.w);
+    r.x = bilerp(ly0, ly1, lx0, lx1, v00.x, v01.x, v10.x, v11.x);
+    r.y = bilerp(ly0, ly1, lx0, lx1, v00.y, v01.y, v10.y, v11.y);
+    r.z = bilerp(ly0, ly1, lx0, lx1, v00.z, v01.z, v10.z, v11.z);
+    r.w = bilerp(ly0, ly1, lx0, lx1, v00.w, v01.w, v10.w, v11.w);
     *(float4 *)(up + (size_t)pix * C + 4 * q) = r;
 }
 

@@ -54,6 +54,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_EXP_SMALLSTORE
 #define CISTA_EXP_SMALLSTORE 0     // != 0: store offsets masked into a small window (value = mask)
 #endif
+// A/B switches: CISTA_PRIO=1 raises the wave priority around each tap's MFMA cluster;
+// CISTA_NT=1 makes the epilogue's burst stores non-temporal
+#ifndef CISTA_PRIO
+#define CISTA_PRIO 0
+#endif
+#ifndef CISTA_NT
+#define CISTA_NT 0
+#endif
 // Design switch (A/B builds: scripts/build_variants.sh): XCD-aware workgroup order of the conv
 // kernels (0: plain grid order; 1 measured 1 % faster per frame)
 #ifndef CISTA_XCD
@@ -112,6 +120,13 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
 }
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+__device__ __forceinline__ float bilerp(float ly0, float ly1, float lx0, float lx1, float x00, float x01, float x10,
+                                        float x11) {
+    const float t0 = __fadd_rn(__fmul_rn(lx0, x00), __fmul_rn(lx1, x01));
+    const float t1 = __fadd_rn(__fmul_rn(lx0, x10), __fmul_rn(lx1, x11));
+    return __fadd_rn(__fmul_rn(ly0, t0), __fmul_rn(ly1, t1));
+}
 
 // torch.relu: NaN stays NaN (fmaxf alone would map it to 0 and hide an upstream overflow)
 __device__ __forceinline__ float relu_(float x) { return x != x ? x : fmaxf(x, 0.0f); }
@@ -174,11 +189,14 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
             const float4 a01 = *(const float4 *)(p01 + 4 * h);
             const float4 a10 = *(const float4 *)(p10 + 4 * h);
             const float4 a11 = *(const float4 *)(p11 + 4 * h);
-            // torch order: h0l*(w0l*x00 + w1l*x01) + h1l*(w0l*x10 + w1l*x11)
-            r[4 * h + 0] = ly0 * (lx0 * a00.x + lx1 * a01.x) + ly1 * (lx0 * a10.x + lx1 * a11.x);
-            r[4 * h + 1] = ly0 * (lx0 * a00.y + lx1 * a01.y) + ly1 * (lx0 * a10.y + lx1 * a11.y);
-            r[4 * h + 2] = ly0 * (lx0 * a00.z + lx1 * a01.z) + ly1 * (lx0 * a10.z + lx1 * a11.z);
-            r[4 * h + 3] = ly0 * (lx0 * a00.w + lx1 * a01.w) + ly1 * (lx0 * a10.w + lx1 * a11.w);
+            // torch order: h0l*(w0l*x00 + w1l*x01) + h1l*(w0l*x10 + w1l*x11), every operation
+            // rounded on its own: with the compiler free to contract, different instantiations
+            // of this kernel (tile configurations) formed different FMAs, so a sample's frame
+            // depended on the batch size it was run in
+            r[4 * h + 0] = bilerp(ly0, ly1, lx0, lx1, a00.x, a01.x, a10.x, a11.x);
+            r[4 * h + 1] = bilerp(ly0, ly1, lx0, lx1, a00.y, a01.y, a10.y, a11.y);
+            r[4 * h + 2] = bilerp(ly0, ly1, lx0, lx1, a00.z, a01.z, a10.z, a11.z);
+            r[4 * h + 3] = bilerp(ly0, ly1, lx0, lx1, a00.w, a01.w, a10.w, a11.w);
         }
         v0 = make_float4(r[0], r[1], r[2], r[3]);
         v1 = make_float4(r[4], r[5], r[6], r[7]);
@@ -486,7 +504,13 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 // do not include them (vmcnt is in order); they land under taps 0..1
                 if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
                     stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1);
+#if CISTA_PRIO == 1
+                __builtin_amdgcn_s_setprio(1);
+#endif
                 mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
+#if CISTA_PRIO == 1
+                __builtin_amdgcn_s_setprio(0);
+#endif
                 if (tap < 8) {
 #pragma unroll
                     for (int n = 0; n < NW; ++n) {
@@ -834,7 +858,14 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #if CISTA_EXP_SMALLSTORE
                 *(float4 *)(a.out0 + (((unsigned)off + (unsigned)ch) & (unsigned)CISTA_EXP_SMALLSTORE)) = res[m][it];
 #else
+#if CISTA_NT
+                {
+                    const f32x4 r4 = {res[m][it].x, res[m][it].y, res[m][it].z, res[m][it].w};
+                    __builtin_nontemporal_store(r4, (f32x4 *)(a.out0 + (unsigned)off + (unsigned)ch));
+                }
+#else
                 *(float4 *)(a.out0 + (unsigned)off + (unsigned)ch) = res[m][it];
+#endif
 #endif
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
             }

@@ -151,13 +151,27 @@ __global__ void vox_accum_kernel(const unsigned long long *keys, const int *vals
 
 __device__ __forceinline__ float hot(float v, float thr) { return (thr > 0.0f && fabsf(v) > thr) ? 0.0f : v; }
 
-// numpy pairwise_sum leaf (n <= 128) of f(v) and f(v)^2
-__device__ void leaf_sums(const float *a, int n, float thr, float &s, float &q) {
+__device__ __forceinline__ int pw_split(int n) {
+    int n2 = n / 2;
+    return n2 - n2 % 8;
+}
+
+// The chunk is first staged into LDS with coalesced loads (one element per thread per step,
+// hot-pixel filter applied), then every leaf is summed by its own thread from LDS.  Leaf l of
+// the LDS image starts at l * LSTRIDE: a stride of 129 floats puts the 128-element leaves of
+// consecutive threads on consecutive banks (conflict-free), and element i lives at
+// (i >> 7) * LSTRIDE + (i & 127) for any leaf boundary of a partial chunk.
+constexpr int LSTRIDE = LEAF + 1;
+
+__device__ __forceinline__ float lds_at(const float *buf, int i) { return buf[(i >> 7) * LSTRIDE + (i & 127)]; }
+
+// numpy pairwise_sum leaf (n <= 128) of v and v^2 over LDS elements [s, s + n) (already filtered)
+__device__ void leaf_sums_lds(const float *buf, int s0, int n, float &s, float &q) {
     if (n < 8) {
         s = -0.0f;
         q = -0.0f;
         for (int i = 0; i < n; ++i) {
-            const float v = hot(a[i], thr);
+            const float v = lds_at(buf, s0 + i);
             s += v;
             q += v * v;
         }
@@ -166,14 +180,14 @@ __device__ void leaf_sums(const float *a, int n, float thr, float &s, float &q) 
     float r[8], rq[8];
 #pragma unroll
     for (int k = 0; k < 8; ++k) {
-        r[k] = hot(a[k], thr);
+        r[k] = lds_at(buf, s0 + k);
         rq[k] = r[k] * r[k];
     }
     int i = 8;
     for (; i < n - (n % 8); i += 8) {
 #pragma unroll
         for (int k = 0; k < 8; ++k) {
-            const float v = hot(a[i + k], thr);
+            const float v = lds_at(buf, s0 + i + k);
             r[k] += v;
             rq[k] += v * v;
         }
@@ -181,20 +195,16 @@ __device__ void leaf_sums(const float *a, int n, float thr, float &s, float &q) 
     s = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     q = ((rq[0] + rq[1]) + (rq[2] + rq[3])) + ((rq[4] + rq[5]) + (rq[6] + rq[7]));
     for (; i < n; ++i) {
-        const float v = hot(a[i], thr);
+        const float v = lds_at(buf, s0 + i);
         s += v;
         q += v * v;
     }
 }
 
-__device__ __forceinline__ int pw_split(int n) {
-    int n2 = n / 2;
-    return n2 - n2 % 8;
-}
-
 // grid (nchunks, B), block MAX_LEAVES
 __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox, long long n, int nchunks,
                                                                float thr, ChunkPart *parts) {
+    __shared__ float buf[(CHUNK / LEAF) * LSTRIDE];
     __shared__ int lstart[MAX_LEAVES], llen[MAX_LEAVES];
     __shared__ float ls[MAX_LEAVES], lq[MAX_LEAVES];
     __shared__ int rcnt[MAX_LEAVES];
@@ -221,18 +231,31 @@ __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox,
         }
         nleaves = nl;
     }
-    // count / min / max: order-independent
+    // coalesced staging + count / min / max (order-independent)
     int cnt = 0;
     float mn = INFINITY, mx = -INFINITY;
-    for (int i = tid; i < m; i += MAX_LEAVES) {
-        const float v = hot(a[i], thr);
-        cnt += v != 0.0f;
-        mn = fminf(mn, v);
-        mx = fmaxf(mx, v);
+    constexpr int U = 8;
+    for (int i0 = tid; i0 < m; i0 += U * MAX_LEAVES) {
+        float v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * MAX_LEAVES;
+            v[u] = i < m ? hot(a[i], thr) : 0.0f;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int i = i0 + u * MAX_LEAVES;
+            if (i < m) {
+                buf[(i >> 7) * LSTRIDE + (i & 127)] = v[u];
+                cnt += v[u] != 0.0f;
+                mn = fminf(mn, v[u]);
+                mx = fmaxf(mx, v[u]);
+            }
+        }
     }
     rcnt[tid] = cnt; rmn[tid] = mn; rmx[tid] = mx;
     __syncthreads();
-    if (tid < nleaves) leaf_sums(a + lstart[tid], llen[tid], thr, ls[tid], lq[tid]);
+    if (tid < nleaves) leaf_sums_lds(buf, lstart[tid], llen[tid], ls[tid], lq[tid]);
     for (int k = MAX_LEAVES / 2; k > 0; k >>= 1) {
         if (tid < k) {
             rcnt[tid] += rcnt[tid + k];
