@@ -21,7 +21,7 @@ inline size_t align_up(size_t x) { return (x + ALIGN - 1) & ~(ALIGN - 1); }
 // ---------------------------------------------------------------------------------------
 // packed parameter blob layout
 // ---------------------------------------------------------------------------------------
-enum ConvId { CV_W0, CV_P0, CV_GATES, CV_OUTG, CV_D, CV_P, CV_DG, CV_LSTM, CV_UP, CV_IN, CV_COUNT };
+enum ConvId { CV_W0, CV_P0, CV_GATES, CV_OUTG, CV_D, CV_P, CV_DG, CV_LSTM, CV_UP, CV_IN, CV_UP4, CV_COUNT };
 
 struct ConvShape { int cout, cin, G; };
 
@@ -36,6 +36,7 @@ ConvShape conv_shape(int id, int C) {
         case CV_DG: return {C, 2 * C, 1};
         case CV_LSTM: return {4 * C, 2 * C, 4};      // (in, remember, out, cell) base_layers.py:116
         case CV_IN: return {C, 32, 1};               // composed input stage + W0 over the s2d input
+        case CV_UP4: return {4 * C, C, 1};           // phase-decomposed upsample conv (4 phases x C)
         default: return {C, C, 1};                   // CV_UP
     }
 }
@@ -43,7 +44,7 @@ ConvShape conv_shape(int id, int C) {
 struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
-    size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS;
+    size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS, wU4, bU4, wUT, bU;
     size_t total;
 };
 
@@ -77,6 +78,10 @@ Layout make_layout(const cista_config &cfg) {
     L.bC = off; off = align_up(off + (size_t)C * 4);
     L.wS = off; off = align_up(off + (size_t)C * 32 * 9 * 4);            // CV_IN, reference layout
     L.bS = off; off = align_up(off + (size_t)C * 4);
+    L.wU4 = off; off = align_up(off + (size_t)4 * C * C * 9 * 4);        // CV_UP4, reference layout
+    L.bU4 = off; off = align_up(off + (size_t)4 * C * 4);
+    L.wUT = off; off = align_up(off + (size_t)C * C * 9 * 4);            // upsample W as [ci*9+t][co]
+    L.bU = off; off = align_up(off + (size_t)C * 4);
     L.total = off;
     return L;
 }
@@ -186,7 +191,11 @@ template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF =
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
-    const Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC);
+    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC);
+    if (a.border == 1)          // rows 0 and Hout-1 in 1-row tiles
+        t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S)};
+    else if (a.border == 2)     // columns 0 and Wout-1 in 1-column tiles
+        t = Tile{block_px, 1, (a.Hout + block_px - 1) / block_px, 2, lds_bytes(block_px, 1, S)};
     a.TH = t.TH;
     a.TW = t.TW;
     a.tiles_y = t.ty;
@@ -262,13 +271,17 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         if (a.N % 64 == 0) return launch_conv_cfg<2, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N % 32 == 0) return launch_conv_cfg<2, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
+    } else if constexpr (EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE) {
+        // one wave per phase (NW * 16 == C columns), 96 half-res pixels x 4 phases per workgroup
+        if (a.N == 256 && a.Cout == 64) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
+        return CISTA_ERR_UNSUPPORTED;
     } else if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE) {      // needs WN == 1
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2)) {
+    } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_S2D)) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
-        constexpr bool FWD = STAGE == STAGE_S1;
+        constexpr bool FWD = STAGE == STAGE_S1 || STAGE == STAGE_S2D;
         if constexpr (FWD) {
             // small batches (B = 1 is the reference harness's case): the throughput tiles below
             // leave most CUs idle, so 64-pixel x 64-column workgroups trade MFMA efficiency
@@ -373,9 +386,21 @@ inline bool fused_input(const cista_config &cfg) { return CISTA_FUSED_IN && cfg.
 #endif
 // ... with its interior on MFMA (space-to-depth input, 4 (nb+1) <= 32 channels)
 inline bool s2d_input(const cista_config &cfg) { return CISTA_S2D_IN && cfg.num_bins <= 7; }
+// ... staged straight from the NCHW planes by the conv (no s2d tensor round trip through HBM)
+#ifndef CISTA_S2D_DIRECT
+#define CISTA_S2D_DIRECT 1
+#endif
 
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
+// ... and for C = 64 it runs phase-decomposed over the half-res input
+#ifndef CISTA_UP4
+#define CISTA_UP4 1
+#endif
+inline bool up4_path(int C) { return CISTA_UP4 && C == 64; }
+#ifndef CISTA_UP4_BORDER_VALU
+#define CISTA_UP4_BORDER_VALU 0   // 1: the border pixels by up_border_kernel (VALU) instead
+#endif
 
 ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int Hout, int Wout,
                      const float *in0, int c0, const float *in1, int c1) {
@@ -398,7 +423,18 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 fa.out = f.x1; fa.B = B; fa.H = f.H; fa.W = f.W; fa.h = h; fa.w = w; fa.C = C;
                 fa.border_only = 0;
                 long most = (long)B * (h > 2 ? h - 2 : 1) * (w > 2 ? w - 2 : 1);
-                if (s2d_input(*f.cfg)) {
+                if (s2d_input(*f.cfg) && CISTA_S2D_DIRECT) {
+                    // interior on MFMA, the space-to-depth view staged straight from the NCHW
+                    // planes (STAGE_S2D); the padded border outputs are then overwritten by the
+                    // VALU pass
+                    a = conv_args_f(f, CV_IN, C, B, h, w, h, w, f.events, 32, nullptr, 0);
+                    a.s2d_img = f.prev_image;
+                    a.s2d_nb = f.cfg->num_bins;
+                    a.out0 = f.x1;
+                    if (const int sc = launch_conv<STAGE_S2D, EPI_BIAS, 1>(a, f.st)) return sc;
+                    fa.border_only = 1;
+                    most = (long)B * (h > w ? h : w);
+                } else if (s2d_input(*f.cfg)) {
                     // interior on MFMA: s2d input (in x_full's space) -> 3x3 split-f16 conv; the
                     // conv's reflect-padded border outputs are then overwritten by the VALU pass
                     const dim3 gs((unsigned)(((long)B * h * w + 255) / 256));
@@ -492,6 +528,37 @@ int run_layer(const Frame &f, int layer, int it = 0) {
             a.out0 = f.hs; a.out1 = f.cs; a.aux0 = f.c_prev; a.out2 = f.lg;
             return launch_conv<STAGE_S1, EPI_LSTM, 4>(a, f.st);
         case CISTA_LAYER_UPSAMPLE:  // relu(conv(ReflectionPad(up2x(h))))          :193-210
+            if (up4_path(C)) {
+                // phase-decomposed: one 4C-column conv over the half-res h (edge-replicated),
+                // then the exact border pass for full-res rows 0, H-1 and columns 0, W-1
+                a = conv_args_f(f, CV_UP4, C, B, h, w, h, w, f.hs, C, nullptr, 0);
+                a.Cout = C;
+                a.out0 = f.full; a.aux0 = blob<float>(f.packed, f.L.wF); a.out1 = f.u;
+                const int sc = f.u ? launch_conv<STAGE_CLAMP, EPI_UP4_Q_SAVE, 1>(a, f.st)
+                                   : launch_conv<STAGE_CLAMP, EPI_UP4_Q, 1>(a, f.st);
+                if (sc) return sc;
+#if CISTA_UP4_BORDER_VALU
+                UpBorderArgs ub;
+                ub.h = f.hs; ub.wt = blob<float>(f.packed, f.L.wUT); ub.bias = blob<float>(f.packed, f.L.bU);
+                ub.wf = blob<float>(f.packed, f.L.wF);
+                ub.q = f.full; ub.u = f.u; ub.B = B; ub.H = f.H; ub.W = f.W; ub.C = C;
+                const long nbp = (long)B * (2 * f.W + 2 * (f.H - 2));
+                hipLaunchKernelGGL(up_border_kernel, dim3((unsigned)nbp), dim3(64), (size_t)9 * C * 4, f.st, ub);
+                return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+#else
+                // border strips: the bilinear-staging upsample conv (exact reference arithmetic)
+                // on 1-row / 1-column tiles, one fixed configuration for every batch size
+                for (int mode = 1; mode <= 2; ++mode) {
+                    ConvArgs bo = conv_args_f(f, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
+                    bo.out0 = f.full; bo.aux0 = blob<float>(f.packed, f.L.wF); bo.out1 = f.u;
+                    bo.border = mode;
+                    const int sb = f.u ? launch_conv_cfg<2, 4, 4, 1, STAGE_UP, EPI_UP_Q_SAVE, 1>(bo, f.st)
+                                       : launch_conv_cfg<2, 4, 4, 1, STAGE_UP, EPI_UP_Q, 1>(bo, f.st);
+                    if (sb) return sb;
+                }
+                return CISTA_OK;
+#endif
+            }
             a = conv_args_f(f, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
             a.out0 = f.full;
             if (up_q_path(C)) {     // + final_conv's channel contraction in the epilogue
@@ -1067,10 +1134,17 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
                            (const float *)blobw<float>(packed, L.wC), (const float *)blobw<float>(packed, L.bC),
                            blobw<float>(packed, L.wS), blobw<float>(packed, L.bS), nb, C);
     }
+    {
+        const int nu = 4 * C * C * 9 + 4 * C;
+        hipLaunchKernelGGL(compose_up4_kernel, dim3((nu + 255) / 256), dim3(256), 0, st, p->up_w, p->up_b,
+                           blobw<float>(packed, L.wU4), blobw<float>(packed, L.bU4), C);
+    }
     const float *ws[CV_COUNT] = {p->W0_w, p->P0_w, p->gates_w, p->out_gates_w, p->D_w, p->P_w,
-                                 p->Dg_w, p->lstm_w, p->up_w, blobw<float>(packed, L.wS)};
+                                 p->Dg_w, p->lstm_w, p->up_w, blobw<float>(packed, L.wS),
+                                 blobw<float>(packed, L.wU4)};
     const float *bs[CV_COUNT] = {p->W0_b, p->P0_b, p->gates_b, p->out_gates_b, p->D_b, p->P_b,
-                                 p->Dg_b, p->lstm_b, p->up_b, blobw<float>(packed, L.bS)};
+                                 p->Dg_b, p->lstm_b, p->up_b, blobw<float>(packed, L.bS),
+                                 blobw<float>(packed, L.bU4)};
     for (int i = 0; i < CV_COUNT; ++i) {
         const ConvShape s = conv_shape(i, C);
         PackArgs a;
@@ -1099,11 +1173,14 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
                        p->Wi_w, blobw<float>(packed, L.wI), half, 1);
     hipLaunchKernelGGL(final_weight_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st,
                        p->final_w, blobw<float>(packed, L.wF), C);
+    hipLaunchKernelGGL(transpose_small_kernel, dim3((C * C * 9 + 255) / 256), dim3(256), 0, st,
+                       p->up_w, blobw<float>(packed, L.wUT), C, C);
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     char *pb = static_cast<char *>(packed);
     if (hipMemcpyAsync(pb + L.bIn, p->We_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.bIn + half * 4, p->Wi_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.bF, p->final_b, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+        hipMemcpyAsync(pb + L.bU, p->up_b, (size_t)C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.lambda, p->lambda, 2 * C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return CISTA_ERR_HIP;
     return CISTA_OK;

@@ -69,7 +69,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #endif
 
 
-enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2, STAGE_ZP2 = 3 };
+// STAGE_CLAMP: stride 1 with edge-replicate padding (the phase-decomposed upsample conv reads
+// the half-resolution h; bilinear's index clamping is edge replication, base_layers.py:198)
+// STAGE_S2D: the composed input stage's interior conv reads the 2x2 space-to-depth view of the
+// NCHW event planes + previous image straight from them (no s2d tensor in HBM): half-res pixel
+// (Y, X), channel s = plane * 4 + (py * 2 + px) -> plane[2Y + py][2X + px]; planes >= nb + 1 are 0
+enum Stage { STAGE_S1 = 0, STAGE_S2 = 1, STAGE_UP = 2, STAGE_ZP2 = 3, STAGE_CLAMP = 4, STAGE_S2D = 5 };
 enum Epi {
     EPI_BIAS = 0,        // out = acc + b
     EPI_RELU = 1,        // out = relu(acc + b)
@@ -81,7 +86,11 @@ enum Epi {
     EPI_UP_Q = 7,        // u = relu(acc + b) -> q_t = sum_c u_c * wf[t][c], t = 0..8: the
                          // final_conv (64->1) contracted over channels in the epilogue, so u
                          // never reaches HBM; the 9 shifted taps are summed by final_q_kernel
-    EPI_UP_Q_SAVE = 8    // EPI_UP_Q that also stores u (out1) for the training backward
+    EPI_UP_Q_SAVE = 8,   // EPI_UP_Q that also stores u (out1) for the training backward
+    EPI_UP4_Q = 9,       // EPI_UP_Q of the phase-decomposed upsample conv: the output columns are
+                         // (phase a*2+b, channel); a half-res pixel (i, j) yields u at the
+                         // full-res pixel (2i+a, 2j+b) -- the q planes are full resolution
+    EPI_UP4_Q_SAVE = 10  // ... and stores u (out1, full-res NHWC)
 };
 
 struct ConvArgs {
@@ -108,6 +117,10 @@ struct ConvArgs {
     float *out2;
     const float *ascale; // optional [2]: {s, 1/s} power-of-two input pre-scale (dgrad inputs)
     int *rflag;          // optional: set to 1 when a staged |x| >= 65504 (fp16 split range)
+    int border;          // 0, or the border-strip tiling (see the kernel's tile origin)
+    // STAGE_S2D: in0 = events (B, s2d_nb, 2Hin, 2Win), s2d_img = prev image (B, 1, 2Hin, 2Win)
+    const float *s2d_img;
+    int s2d_nb;
 };
 
 __device__ __forceinline__ int reflect_clamp(int i, int n) {
@@ -309,6 +322,14 @@ __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, 
             if constexpr (STAGE == STAGE_ZP2) {
                 const int iy = iy0 + hy, ix = ix0 + hx;
                 pix = (iy < 0 || iy >= a.Hin || ix < 0 || ix >= a.Win) ? -2 : (b * a.Hin + iy) * a.Win + ix;
+            } else if constexpr (STAGE == STAGE_CLAMP) {
+                const int iy = min(max(iy0 + hy, 0), a.Hin - 1), ix = min(max(ix0 + hx, 0), a.Win - 1);
+                pix = (b * a.Hin + iy) * a.Win + ix;
+            } else if constexpr (STAGE == STAGE_S2D) {
+                // clamped: the outputs the padding feeds (the border rows / columns) are
+                // overwritten by the exact VALU border pass
+                const int iy = min(max(iy0 + hy, 0), a.Hin - 1), ix = min(max(ix0 + hx, 0), a.Win - 1);
+                pix = (2 * iy) * (2 * a.Win) + 2 * ix;            // in-plane offset of (2Y, 2X)
             } else {
                 const int iy = reflect_clamp(iy0 + hy, a.Hin), ix = reflect_clamp(ix0 + hx, a.Win);
                 pix = (b * a.Hin + iy) * a.Win + ix;
@@ -321,7 +342,31 @@ __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, 
 template <int STAGE, int NI>
 __device__ __forceinline__ void stage_issue_px(const ConvArgs &a, const float *seg, int segC, int choff,
                                                const int (&spix)[NI], const int (&gs)[NI], float4 (&v0)[NI],
-                                               float4 (&v1)[NI]) {
+                                               float4 (&v1)[NI], int b = 0) {
+    if constexpr (STAGE == STAGE_S2D) {
+        // item (pixel, g): planes 2g and 2g+1, each as two float2 rows of its 2x2 block
+        const int Wf = 2 * a.Win;
+        const size_t plane = (size_t)(2 * a.Hin) * Wf;
+#pragma unroll
+        for (int u = 0; u < NI; ++u) {
+            const int o = spix[u] < 0 ? 0 : spix[u];
+            float2 q[4];
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const int pl = 2 * gs[u] + k;
+                const float *src = pl < a.s2d_nb ? seg + ((size_t)b * a.s2d_nb + pl) * plane
+                                                 : a.s2d_img + (size_t)b * plane;
+                const bool live = pl <= a.s2d_nb;
+                const float2 r0 = live ? *(const float2 *)(src + o) : make_float2(0.f, 0.f);
+                const float2 r1 = live ? *(const float2 *)(src + o + Wf) : make_float2(0.f, 0.f);
+                q[2 * k] = r0;
+                q[2 * k + 1] = r1;
+            }
+            v0[u] = make_float4(q[0].x, q[0].y, q[1].x, q[1].y);
+            v1[u] = make_float4(q[2].x, q[2].y, q[3].x, q[3].y);
+        }
+        return;
+    }
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         const int pix = spix[u];
@@ -411,7 +456,10 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     t /= a.tiles_x;
     const int ty = t % a.tiles_y;
     const int b = t / a.tiles_y;
-    const int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    // border strips (a.border != 0): 1-row tiles on output rows 0 and Hout-1 (1), or 1-column
+    // tiles on columns 0 and Wout-1 (2) -- the phase-decomposed upsample's exact border pass
+    const int oy0 = a.border == 1 ? (ty ? a.Hout - 1 : 0) : ty * a.TH;
+    const int ox0 = a.border == 2 ? (tx ? a.Wout - 1 : 0) : tx * a.TW;
 
     constexpr int S = (STAGE == STAGE_S2) ? 2 : 1;
     const int HWd = (a.TW - 1) * S + 3;
@@ -455,15 +503,16 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     };
     if constexpr (NI > 0) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
-        static_assert(STAGE == STAGE_S1 || STAGE == STAGE_S2 || STAGE == STAGE_ZP2,
-                      "double-buffered staging: direct (reflect / zero padded) inputs");
+        static_assert(STAGE == STAGE_S1 || STAGE == STAGE_S2 || STAGE == STAGE_ZP2 || STAGE == STAGE_CLAMP ||
+                          STAGE == STAGE_S2D,
+                      "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
         stage_pixels<STAGE, NI>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
         {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
             float4 sv0[NI], sv1[NI];
-            stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1);
+            stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1, b);
             stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
         }
         __syncthreads();
@@ -503,7 +552,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 // the next chunk's halo loads go out after B(0), B(1): the waits for those two
                 // do not include them (vmcnt is in order); they land under taps 0..1
                 if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
-                    stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1);
+                    stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
 #if CISTA_PRIO == 1
                 __builtin_amdgcn_s_setprio(1);
 #endif
@@ -594,8 +643,15 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
 
-    if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE) {
-        static_assert(WN == 1, "the wave must hold every output channel");
+    if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE || EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE) {
+        constexpr bool PH4 = EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE;
+        constexpr bool SAVE_U = EPI == EPI_UP_Q_SAVE || EPI == EPI_UP4_Q_SAVE;
+        static_assert(PH4 || WN == 1, "the wave must hold every output channel");
+        // phase-decomposed: the wave's NW*16 columns are all the channels of one phase
+        const int phase = PH4 ? (nt0 * 16) / a.Cout : 0;
+        const int c0 = PH4 ? nt0 * 16 - phase * a.Cout : nt0 * 16;   // first channel of the wave
+        const int Hq = PH4 ? 2 * a.Hout : a.Hout, Wq = PH4 ? 2 * a.Wout : a.Wout;   // q / u planes
+        const int pa = phase >> 1, pb = phase & 1;
         // values v[t*4 + j] (tap t, accumulator row j) of this lane's channel subset, then a
         // reduce-scatter over the 16 lanes (columns) of each row group: after halving 48 -> 3,
         // lane `col` holds the channel sums of value indices 3*col .. 3*col+2.
@@ -616,16 +672,18 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
             for (int i = 0; i < 48; ++i) v[i] = 0.0f;
 #pragma unroll
             for (int n = 0; n < NW; ++n) {
-                const float *wf = wfs + (nt0 + n) * 16 + col;
+                const float *wf = wfs + c0 + n * 16 + col;
 #pragma unroll
                 for (int j = 0; j < 4; ++j) {
                     const float u = relu_(acc[m][n][j] + bz[n]);
-                    if constexpr (EPI == EPI_UP_Q_SAVE) {   // keep u for the final_conv / ReLU backward
+                    if constexpr (SAVE_U) {   // keep u for the final_conv / ReLU backward
                         const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
                         const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
-                        if (p < npix && oy0 + py < a.Hout && ox0 + px < a.Wout)
-                            a.out1[(((size_t)b * a.Hout + oy0 + py) * a.Wout + ox0 + px) * a.Cout +
-                                   (nt0 + n) * 16 + col] = u;
+                        if (p < npix && oy0 + py < a.Hout && ox0 + px < a.Wout) {
+                            const int Y = PH4 ? 2 * (oy0 + py) + pa : oy0 + py;
+                            const int X = PH4 ? 2 * (ox0 + px) + pb : ox0 + px;
+                            a.out1[(((size_t)b * Hq + Y) * Wq + X) * a.Cout + c0 + n * 16 + col] = u;
+                        }
                     }
 #pragma unroll
                     for (int t = 0; t < 9; ++t) v[t * 4 + j] = fmaf(u, wf[t * a.Cout], v[t * 4 + j]);
@@ -652,7 +710,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 const int px = p - py * a.TW;
                 const int oy = oy0 + py, ox = ox0 + px;
                 if (oy >= a.Hout || ox >= a.Wout) continue;
-                a.out0[(((size_t)b * 9 + t) * a.Hout + oy) * a.Wout + ox] = v[r];
+                const int Y = PH4 ? 2 * oy + pa : oy, X = PH4 ? 2 * ox + pb : ox;
+                a.out0[(((size_t)b * 9 + t) * Hq + Y) * Wq + X] = v[r];
             }
         }
         return;
@@ -1156,8 +1215,8 @@ __global__ __launch_bounds__(256) void s2d_input_kernel(const float *events, con
 #pragma unroll
         for (int py = 0; py < 2; ++py) {
             const float2 q = *(const float2 *)(src + (size_t)(2 * Y + py) * W + 2 * X);
-            v[(py * 2) * K + ci] = q.x;
-            v[(py * 2 + 1) * K + ci] = q.y;
+            v[ci * 4 + py * 2] = q.x;               // s = plane * 4 + phase (STAGE_S2D order)
+            v[ci * 4 + py * 2 + 1] = q.y;
         }
     }
     float4 *o = (float4 *)(out + pix * 32);
@@ -1177,7 +1236,7 @@ __global__ void s2d_weight_kernel(const float *E, const float *bC, float *Ws, fl
     const int tap = idx % 9, s = (idx / 9) % 32, co = idx / (9 * 32);
     float v = 0.f;
     if (s < 4 * K) {
-        const int ph = s / K, ci = s - ph * K;
+        const int ph = s & 3, ci = s >> 2;               // s = plane * 4 + phase (STAGE_S2D order)
         const int offy = 2 * (tap / 3 - 1) + (ph >> 1), offx = 2 * (tap % 3 - 1) + (ph & 1);
         if (offy <= 2 && offx <= 2)
             v = E[((size_t)(4 * 25 + (offy + 2) * 5 + (offx + 2)) * K + ci) * C + co];
@@ -1255,6 +1314,101 @@ __global__ __launch_bounds__(256) void final_stage_kernel(const FinalArgs a) {
     const float pre = acc + a.bias[0];
     if (a.pre) a.pre[pix] = pre;
     a.rec[pix] = sigmoidf_(pre);
+}
+
+// ------------------------------------------------------------------------------------------
+// Phase-decomposed upsample conv (base_layers.py:193-210).  Bilinear x2 (align_corners=False)
+// then a 3x3 conv is linear: full-res output row 2i+a, tap dy reads upsampled row 2i+a+dy-1,
+// which is 0.75/0.25 (or 0.25/0.75) of half-res rows i-1, i, i+1.  So every output phase (a, b)
+// is a 3x3 conv over the half-res h with composed weights
+//   W4[a*2+b][co][ci][r][s] = sum_{dy,dx} W[co][ci][dy][dx] A[a][dy][r] A[b][dx][s],
+// N = 4C columns of one implicit GEMM, with NO per-pixel interpolation.  Bilinear's index clamp
+// is edge replication of h (STAGE_CLAMP).  ReflectionPad2d(1) of the full-res image is not
+// expressible that way: the output rows 0, H-1 and columns 0, W-1 are recomputed exactly by
+// up_border_kernel after the conv.
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ double up_phase_w(int a, int d, int r) {
+    // A[a][d][r]: weight of half-res row i + r - 1 in upsampled row 2i + a + d - 1
+    const double t[2][3][3] = {{{0.75, 0.25, 0.0}, {0.25, 0.75, 0.0}, {0.0, 0.75, 0.25}},
+                               {{0.25, 0.75, 0.0}, {0.0, 0.75, 0.25}, {0.0, 0.25, 0.75}}};
+    return t[a][d][r];
+}
+
+// W4 [4C][C][3][3] (reference layout, packed like every conv) and the bias b4 [4C]
+__global__ void compose_up4_kernel(const float *W, const float *b, float *W4, float *b4, int C) {
+    const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= 4 * C * C * 9 + 4 * C) return;
+    if (idx >= 4 * C * C * 9) {
+        const int o = idx - 4 * C * C * 9;
+        b4[o] = b[o % C];
+        return;
+    }
+    const int tap = idx % 9, ci = (idx / 9) % C, oc = idx / (9 * C);
+    const int phase = oc / C, co = oc % C, pa = phase >> 1, pb = phase & 1, r = tap / 3, sx = tap % 3;
+    double acc = 0.0;
+    for (int dy = 0; dy < 3; ++dy)
+        for (int dx = 0; dx < 3; ++dx)
+            acc += (double)W[((size_t)co * C + ci) * 9 + dy * 3 + dx] * up_phase_w(pa, dy, r) * up_phase_w(pb, dx, sx);
+    W4[idx] = (float)acc;
+}
+
+// Border pixels of the upsample conv (full-res rows 0, H-1 and columns 0, W-1), the reference
+// arithmetic exactly: bilinear x2 of h at the ReflectionPad2d(1)-mapped positions, the 3x3 conv
+// in fp32, ReLU, then final_conv's 9 per-tap channel contractions (q planes, EPI_UP_Q layout).
+// One 64-thread workgroup per border pixel; thread = output channel(s).
+struct UpBorderArgs {
+    const float *h;      // (B, h, w, C) NHWC
+    const float *wt;     // [C_in * 9 + tap][C_out] (transpose_small_kernel layout: coalesced over co)
+    const float *bias;   // [C]
+    const float *wf;     // [9][C] final_conv weights
+    float *q;            // (B, 9, H, W)
+    float *u;            // optional (B, H, W, C): u for the training backward
+    int B, H, W, C;
+};
+
+__global__ __launch_bounds__(64) void up_border_kernel(const UpBorderArgs a) {
+    extern __shared__ float U[];                    // [9][C] upsampled + reflect-padded window
+    const int nb = 2 * a.W + 2 * (a.H - 2);
+    const int b = blockIdx.x / nb, k = blockIdx.x - (blockIdx.x / nb) * nb;
+    int Y, X;
+    if (k < a.W) { Y = 0; X = k; }
+    else if (k < 2 * a.W) { Y = a.H - 1; X = k - a.W; }
+    else if (k < 2 * a.W + a.H - 2) { Y = 1 + (k - 2 * a.W); X = 0; }
+    else { Y = 1 + (k - 2 * a.W - (a.H - 2)); X = a.W - 1; }
+    const int hh = a.H / 2, ww = a.W / 2, C = a.C;
+    for (int i = threadIdx.x; i < 9 * C; i += 64) {
+        const int t = i / C, c = i - t * C;
+        int Yr = Y + t / 3 - 1, Xr = X + t % 3 - 1;                       // ReflectionPad2d(1)
+        Yr = Yr < 0 ? -Yr : (Yr >= a.H ? 2 * a.H - 2 - Yr : Yr);
+        Xr = Xr < 0 ? -Xr : (Xr >= a.W ? 2 * a.W - 2 - Xr : Xr);
+        const float sy = fmaxf(((float)Yr + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const float sx = fmaxf(((float)Xr + 0.5f) * 0.5f - 0.5f, 0.0f);
+        const int y0 = (int)sy, x0 = (int)sx;
+        const int y1 = y0 + (y0 < hh - 1 ? 1 : 0), x1 = x0 + (x0 < ww - 1 ? 1 : 0);
+        const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1, lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
+        const float *hb = a.h + (size_t)b * hh * ww * C + c;
+        U[i] = bilerp(ly0, ly1, lx0, lx1, hb[((size_t)y0 * ww + x0) * C], hb[((size_t)y0 * ww + x1) * C],
+                      hb[((size_t)y1 * ww + x0) * C], hb[((size_t)y1 * ww + x1) * C]);
+    }
+    __syncthreads();
+    float qv[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int co = threadIdx.x; co < C; co += 64) {
+        float s = 0.0f;
+        for (int ci = 0; ci < C; ++ci)
+#pragma unroll
+            for (int t = 0; t < 9; ++t) s = fmaf(U[t * C + ci], a.wt[(size_t)(ci * 9 + t) * C + co], s);
+        const float u = relu_(s + a.bias[co]);
+        if (a.u) a.u[(((size_t)b * a.H + Y) * a.W + X) * C + co] = u;
+#pragma unroll
+        for (int t = 0; t < 9; ++t) qv[t] = fmaf(u, a.wf[t * C + co], qv[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        float v = qv[t];
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
+        if (threadIdx.x == 0) a.q[(((size_t)b * 9 + t) * a.H + Y) * a.W + X] = v;
+    }
 }
 
 // ------------------------------------------------------------------------------------------
