@@ -210,13 +210,23 @@ __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox,
     __shared__ int rcnt[MAX_LEAVES];
     __shared__ float rmn[MAX_LEAVES], rmx[MAX_LEAVES];
     __shared__ int nleaves;
+    // thread 0's recursion stacks live in LDS: as private arrays with dynamic indices they were
+    // scratch memory, and the serial walks dominated the kernel (4 ms for 960 windows)
+    __shared__ int st_s[32], st_n[32], st_state[32];
+    __shared__ float st_ls[32], st_lq[32];
     const int c = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
     const long long start = (long long)c * CHUNK;
     const int m = (int)((n - start) < CHUNK ? (n - start) : CHUNK);
     const float *a = vox + (size_t)b * n + start;
-    // leaves of numpy's pairwise recursion, left to right
-    if (tid == 0) {
-        int st_s[32], st_n[32], top = 0, nl = 0;
+    // a full chunk's recursion is the balanced tree over 64 leaves of 128 (8192 = 64 * 128 and
+    // every split halves a multiple of 8): leaves and combination are static, done in parallel
+    const bool full = m == CHUNK;
+    static_assert(CHUNK % LEAF == 0 && (CHUNK / LEAF & (CHUNK / LEAF - 1)) == 0, "balanced full chunk");
+    if (full) {
+        if (tid < CHUNK / LEAF) { lstart[tid] = tid * LEAF; llen[tid] = LEAF; }
+        if (tid == 0) nleaves = CHUNK / LEAF;
+    } else if (tid == 0) {      // leaves of numpy's pairwise recursion, left to right
+        int top = 0, nl = 0;
         st_s[top] = 0; st_n[top] = m; ++top;
         while (top > 0) {
             --top;
@@ -264,10 +274,26 @@ __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox,
         }
         __syncthreads();
     }
+    if (full) {
+        // node = left + right, level by level (the same additions as the recursion)
+        for (int k = CHUNK / LEAF / 2; k >= 1; k >>= 1) {
+            __syncthreads();
+            float s2 = 0.0f, q2 = 0.0f;
+            if (tid < k) { s2 = ls[2 * tid] + ls[2 * tid + 1]; q2 = lq[2 * tid] + lq[2 * tid + 1]; }
+            __syncthreads();
+            if (tid < k) { ls[tid] = s2; lq[tid] = q2; }
+        }
+        __syncthreads();
+        if (tid == 0) {
+            ChunkPart p;
+            p.sum = ls[0]; p.sq = lq[0]; p.nnz = rcnt[0]; p.mn = rmn[0]; p.mx = rmx[0];
+            parts[(size_t)b * nchunks + c] = p;
+        }
+        return;
+    }
     if (tid == 0) {
         // post-order evaluation of the same recursion: node = left + right
-        int st_n[32], st_state[32], top = 0, leaf = 0;
-        float st_ls[32], st_lq[32];
+        int top = 0, leaf = 0;
         st_n[0] = m; st_state[0] = 0; top = 1;
         float vs = 0.0f, vq = 0.0f;
         bool have = false;   // (vs, vq) holds a finished child value to deliver
