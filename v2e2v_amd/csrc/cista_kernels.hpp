@@ -54,6 +54,10 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_EXP_SMALLSTORE
 #define CISTA_EXP_SMALLSTORE 0     // != 0: store offsets masked into a small window (value = mask)
 #endif
+// CISTA_RANGE_CHECK=0 compiles the fp16-range flag out of the staging (A/B of its cost)
+#ifndef CISTA_RANGE_CHECK
+#define CISTA_RANGE_CHECK 1
+#endif
 // A/B switches: CISTA_PRIO=1 raises the wave priority around each tap's MFMA cluster;
 // CISTA_NT=1 makes the epilogue's burst stores non-temporal
 #ifndef CISTA_PRIO
@@ -149,7 +153,8 @@ __device__ __forceinline__ float softshrink_(float x, float l) { return relu_(x 
 // split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25); hmax
 // keeps the running packed max of |hi|: it reaches inf exactly when a staged |x| >= 65520
 // does not fit the fp16 hi part (the range flag; 4 packed v_pk_max_f16 per 8 values)
-__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, f16x8 &hmax) {
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, f16x2 &hmax) {
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
     f16x8 h, l;
 #pragma unroll
@@ -158,7 +163,15 @@ __device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &
         h[i] = hb;
         l[i] = (_Float16)(v[i] - (float)hb);
     }
-    hmax = __builtin_elementwise_max(hmax, __builtin_elementwise_abs(h));
+    // packed |hi| maxima folded into one register (1 VGPR across the K loop, 4 v_pk_max_f16)
+#if CISTA_RANGE_CHECK
+    const f16x8 ah = __builtin_elementwise_abs(h);
+    const f16x2 m01 = __builtin_elementwise_max(f16x2{ah[0], ah[1]}, f16x2{ah[2], ah[3]});
+    const f16x2 m23 = __builtin_elementwise_max(f16x2{ah[4], ah[5]}, f16x2{ah[6], ah[7]});
+    hmax = __builtin_elementwise_max(hmax, __builtin_elementwise_max(m01, m23));
+#else
+    (void)hmax;
+#endif
     hi = __builtin_bit_cast(u32x4, h);
     lo = __builtin_bit_cast(u32x4, l);
 }
@@ -239,7 +252,7 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
 template <int STAGE>
 __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
                                             int ix0, int HH, int HWd, int HPpad,
-                                            const float *seg, int segC, int choff, f16x8 &amax) {
+                                            const float *seg, int segC, int choff, f16x2 &amax) {
     constexpr int BATCH = STAGE == STAGE_UP ? 2 : 4;
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
@@ -290,7 +303,7 @@ __device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, i
 template <int NI>
 __device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4 (&v0)[NI],
                                              const float4 (&v1)[NI], const int (&hps)[NI],
-                                             const int (&gs)[NI], f16x8 &amax) {
+                                             const int (&gs)[NI], f16x2 &amax) {
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
         if (hps[u] < 0) continue;
@@ -456,10 +469,15 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     t /= a.tiles_x;
     const int ty = t % a.tiles_y;
     const int b = t / a.tiles_y;
-    // border strips (a.border != 0): 1-row tiles on output rows 0 and Hout-1 (1), or 1-column
-    // tiles on columns 0 and Wout-1 (2) -- the phase-decomposed upsample's exact border pass
-    const int oy0 = a.border == 1 ? (ty ? a.Hout - 1 : 0) : ty * a.TH;
-    const int ox0 = a.border == 2 ? (tx ? a.Wout - 1 : 0) : tx * a.TW;
+    // border strips (a.border != 0, bilinear-staging upsample only): 1-row tiles on output rows
+    // 0 and Hout-1 (1), or 1-column tiles on columns 0 and Wout-1 (2) -- the phase-decomposed
+    // upsample's exact border pass.  Compiled into STAGE_UP kernels alone: in the others the
+    // runtime select cost 9 VGPRs and spilled the 247-VGPR ISTA convs.
+    int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    if constexpr (STAGE == STAGE_UP) {
+        if (a.border == 1) oy0 = ty ? a.Hout - 1 : 0;
+        if (a.border == 2) ox0 = tx ? a.Wout - 1 : 0;
+    }
 
     constexpr int S = (STAGE == STAGE_S2) ? 2 : 1;
     const int HWd = (a.TW - 1) * S + 3;
@@ -489,7 +507,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    f16x8 amax = {};     // running max of the staged |hi| parts (range flag, see ConvArgs.rflag)
+    f16x2 amax = {};     // running max of the staged |hi| parts (range flag, see ConvArgs.rflag)
     const int NT = a.N >> 4;
     const int nt0 = (nblk * WN + wn) * NW;
     const int kc0 = a.c0 >> 5;
@@ -627,10 +645,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     }
 
     // an activation beyond the fp16 range of the hi part (or inf): the result is not fp32-faithful
-    if (a.rflag) {
-        _Float16 m = amax[0];
-#pragma unroll
-        for (int i = 1; i < 8; ++i) m = m > amax[i] ? m : amax[i];
+    if (CISTA_RANGE_CHECK && a.rflag) {
+        const _Float16 m = amax[0] > amax[1] ? amax[0] : amax[1];
         if (__builtin_isinf((float)m)) *a.rflag = 1;
     }
 
