@@ -556,10 +556,16 @@ def main():
     tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
     if tfiles:
         try:
-            tl = json.load(open(tfiles[-1]))["layers"].get(dom_name)
-            if tl:
+            import hashlib
+            tj = json.load(open(tfiles[-1]))
+            tl = tj["layers"].get(dom_name)
+            sha = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
+            roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
+            if tl and tj.get("lib_sha256") == sha:
                 roofline["traffic"] = tl["hbm_bytes_per_launch"]
-                roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
+            else:       # measured on another build (or not this kernel): never quote stale bytes
+                roofline["traffic_note"] = ("no PMC traffic of this build's " + dom_name + " kernel in "
+                                            + roofline["traffic_source"])
         except (OSError, ValueError, KeyError):
             pass
 

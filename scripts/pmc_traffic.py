@@ -5,8 +5,11 @@ wide (16 B/lane) coalesced read, which is what every staging / epilogue read of 
 is, so read bytes = 2 * FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both counters
 are in KiB and were collected in separate passes (they cannot share the 4 TCC slots).
 
-usage: python scripts/pmc_traffic.py 'gpurun_out/pmcl_*/run_counter_collection.csv' out.json
+usage: python scripts/pmc_traffic.py 'gpurun_out/pmcl_*/run_counter_collection.csv' out.json [lib.so]
+The library's sha256 is recorded: bench.py only quotes the traffic for the build it measured.
 """
+import hashlib
+import os
 import collections
 import csv
 import glob
@@ -16,7 +19,8 @@ import sys
 
 # (STAGE, EPI) template arguments of conv3x3_split3 -> frame-schedule layer
 CONV_LAYER = {(1, 0): "W0", (0, 0): "P0", (0, 4): "gates", (0, 5): "out_gates", (0, 2): "ista_D",
-              (0, 3): "ista_P", (0, 1): "Dg", (0, 6): "lstm", (2, 7): "upsample", (2, 1): "upsample"}
+              (0, 3): "ista_P", (0, 1): "Dg", (0, 6): "lstm", (4, 9): "upsample", (2, 7): "upsample:border",
+              (2, 1): "upsample", (5, 0): "input+W0:conv"}
 
 
 def layer_of(name):
@@ -38,7 +42,11 @@ def layer_of(name):
     return None, None
 
 
-def main(pattern, out):
+def lib_sha256(path):
+    return hashlib.sha256(open(path, "rb").read()).hexdigest()
+
+
+def main(pattern, out, lib=None):
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     durs = collections.defaultdict(list)
     names = {}
@@ -60,10 +68,12 @@ def main(pattern, out):
                       "mean_dur_us_profiled": round(sum(durs[layer]) / len(durs[layer]), 2),
                       "FETCH_SIZE_KiB": round(fk, 1), "WRITE_SIZE_KiB": round(wk, 1),
                       "hbm_bytes_per_launch": round((2 * fk + wk) * 1024)}
+    lib = lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "v2e2v_amd",
+                              "libcista_hip.so")
     json.dump({"source": pattern, "correction": "read = 2 x FETCH_SIZE (gfx950), KiB -> bytes",
-               "layers": res}, open(out, "w"), indent=1)
+               "lib_sha256": lib_sha256(lib), "layers": res}, open(out, "w"), indent=1)
     print(json.dumps(res, indent=1))
 
 
 if __name__ == "__main__":
-    main(sys.argv[1], sys.argv[2])
+    main(sys.argv[1], sys.argv[2], sys.argv[3] if len(sys.argv) > 3 else None)
