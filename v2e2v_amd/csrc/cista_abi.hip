@@ -131,26 +131,41 @@ Workspace carve(void *ws, int B, int H, int W, int C) {
 // ---------------------------------------------------------------------------------------
 // tile selection
 // ---------------------------------------------------------------------------------------
-struct Tile { int TH, TW, ty, tx; size_t lds; };
+// mseg: 0 = the workgroup's pixels fill its 16-pixel m-tiles in row-major order; > 0 = every
+// tile row is cut into mseg row-aligned m-tiles (the last one partly idle), see ConvArgs.mseg
+struct Tile { int TH, TW, ty, tx; size_t lds; int mseg; };
 
 size_t lds_bytes(int TH, int TW, int S) {
     const int HP = ((TH - 1) * S + 3) * ((TW - 1) * S + 3);
     return (size_t)((HP + 15) & ~15) * 8 * 16;
 }
 
+#ifndef CISTA_MSEG
+#define CISTA_MSEG 1      // row-aligned m-tiles for stride-1 convs (0: row-major only, A/B builds)
+#endif
+
 // max_items: staging items (HP rounded to 8, x4 k-groups) one workgroup may hold in registers
-// (0 = unlimited); nbuf: LDS images (2 for the double-buffered loop)
-Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ = 2) {
-    Tile best{1, 1, Hout, Wout, 0};
+// (0 = unlimited); nbuf: LDS images (2 for the double-buffered loop); seg: row-aligned m-tiles
+// allowed (stride-1 stagings).  Ranking: pixel efficiency (useful / computed pixels) first; at
+// equal efficiency a layout whose m-tile A-fragment reads are bank-conflict free (each m-tile's
+// 16 lanes in one halo row: ds_read_b128 serves 16 lanes of 16 contiguous slots per cycle),
+// then the smaller LDS image.
+Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ = 2, bool seg = false) {
+    Tile best{1, 1, Hout, Wout, 0, 0};
     double best_eff = -1.0;
+    int best_conf = 1;
     size_t best_lds = ~(size_t)0;
     const size_t lds_cap = 160 * 1024 / occ;   // occ workgroups per CU
+    const int mtiles = block_px / 16;
+    for (int mode = 0; mode < ((seg && CISTA_MSEG) ? 2 : 1); ++mode)
     for (int TW = 1; TW <= block_px && TW <= Wout; ++TW) {
 #if CISTA_TW16
         // 16-pixel m-tiles that never wrap a tile row read LDS without bank conflicts
         if (Wout >= 16 && (TW % 16) != 0) continue;
 #endif
-        int TH = block_px / TW;
+        const int mseg = mode ? (TW + 15) / 16 : 0;
+        if (mode && TW % 16 == 0) continue;               // same as row-major
+        int TH = mode ? mtiles / mseg : block_px / TW;
         if (TH > Hout) TH = Hout;
         if (TH < 1) continue;
         auto items = [&](int th) { return ((((th - 1) * S + 3) * ((TW - 1) * S + 3) + 7) & ~7) * 4; };
@@ -160,10 +175,15 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
         if (lds > lds_cap) continue;
         const int ty = (Hout + TH - 1) / TH, tx = (Wout + TW - 1) / TW;
         const double eff = (double)Hout * Wout / ((double)ty * tx * block_px);
-        if (eff > best_eff + 1e-9 || (eff > best_eff - 1e-9 && lds < best_lds)) {
+        // row-major m-tiles that wrap a tile row put two halo rows' slots in one lane group
+        const int conf = (S == 1 && (mode || TW % 16 == 0)) ? 0 : 1;
+        const bool better = eff > best_eff + 1e-9 ||
+                            (eff > best_eff - 1e-9 && (conf < best_conf || (conf == best_conf && lds < best_lds)));
+        if (better) {
             best_eff = eff;
+            best_conf = conf;
             best_lds = lds;
-            best = Tile{TH, TW, ty, tx, lds};
+            best = Tile{TH, TW, ty, tx, lds, mseg};
         }
     }
     return best;
@@ -191,13 +211,15 @@ template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF =
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
-    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC);
+    constexpr bool SEG = STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_CLAMP || STAGE == STAGE_S2D;
+    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC, SEG);
     if (a.border == 1)          // rows 0 and Hout-1 in 1-row tiles
-        t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S)};
+        t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S), 0};
     else if (a.border == 2)     // columns 0 and Wout-1 in 1-column tiles
-        t = Tile{block_px, 1, (a.Hout + block_px - 1) / block_px, 2, lds_bytes(block_px, 1, S)};
+        t = Tile{block_px, 1, (a.Hout + block_px - 1) / block_px, 2, lds_bytes(block_px, 1, S), 0};
     a.TH = t.TH;
     a.TW = t.TW;
+    a.pitch = t.mseg ? 16 * t.mseg : t.TW;
     a.tiles_y = t.ty;
     a.tiles_x = t.tx;
     constexpr int nblk_cols = WN * NW * 16;

@@ -125,7 +125,24 @@ struct ConvArgs {
     // STAGE_S2D: in0 = events (B, s2d_nb, 2Hin, 2Win), s2d_img = prev image (B, 1, 2Hin, 2Win)
     const float *s2d_img;
     int s2d_nb;
+    // m-tile layout of the workgroup tile: workgroup pixel index p (m-tile p / 16, lane p % 16)
+    // is tile pixel (p / pitch, p % pitch).  pitch = TW: the TH x TW pixels fill the m-tiles in
+    // row-major order; pitch = 16 * ceil(TW / 16): every tile row starts a new m-tile (its last
+    // m-tile partly idle), so the 16 lanes of an m-tile read 16 contiguous halo slots -- one
+    // conflict-free ds_read_b128 lane group -- also when TW % 16 != 0
+    int pitch;
 };
+
+// workgroup-local pixel index p -> tile coordinates; false for the idle lanes (beyond the
+// tile), whose (py, px) are clamped to a valid pixel
+__device__ __forceinline__ bool tile_pixel(const ConvArgs &a, int p, int &py, int &px) {
+    py = p / a.pitch;
+    px = p - py * a.pitch;
+    const bool ok = py < a.TH && px < a.TW;
+    py = py < a.TH ? py : a.TH - 1;
+    px = px < a.TW ? px : a.TW - 1;
+    return ok;
+}
 
 __device__ __forceinline__ int reflect_clamp(int i, int n) {
     // padding_mode='reflect' with pad 1: -1 -> 1, n -> n-2; tiles overhanging the image by
@@ -489,15 +506,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     (void)Hsrc;
 
     // per-lane A-fragment base (u32x4 units) of every m-tile, tap (0,0)
-    const int npix = a.TH * a.TW;
     const int kgrp = lane >> 4;
     int abase[MT_W];
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        int p = (wm * MT_W + m) * 16 + (lane & 15);
-        p = p < npix ? p : npix - 1;
-        const int py = p / a.TW;
-        const int px = p - py * a.TW;
+        int py, px;
+        tile_pixel(a, (wm * MT_W + m) * 16 + (lane & 15), py, px);
         abase[m] = kgrp * HPpad + py * S * HWd + px * S;
     }
 
@@ -693,9 +707,9 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 for (int j = 0; j < 4; ++j) {
                     const float u = relu_(acc[m][n][j] + bz[n]);
                     if constexpr (SAVE_U) {   // keep u for the final_conv / ReLU backward
-                        const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
-                        const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
-                        if (p < npix && oy0 + py < a.Hout && ox0 + px < a.Wout) {
+                        int py, px;
+                        const bool in = tile_pixel(a, (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j, py, px);
+                        if (in && oy0 + py < a.Hout && ox0 + px < a.Wout) {
                             const int Y = PH4 ? 2 * (oy0 + py) + pa : oy0 + py;
                             const int X = PH4 ? 2 * (ox0 + px) + pb : ox0 + px;
                             a.out1[(((size_t)b * Hq + Y) * Wq + X) * a.Cout + c0 + n * 16 + col] = u;
@@ -720,10 +734,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 const int idx = 3 * col + r;
                 if (idx >= 36) continue;
                 const int t = idx >> 2, j = idx & 3;
-                const int p = (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j;
-                if (p >= npix) continue;
-                const int py = p / a.TW;
-                const int px = p - py * a.TW;
+                int py, px;
+                if (!tile_pixel(a, (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j, py, px)) continue;
                 const int oy = oy0 + py, ox = ox0 + px;
                 if (oy >= a.Hout || ox >= a.Wout) continue;
                 const int Y = PH4 ? 2 * oy + pa : oy, X = PH4 ? 2 * ox + pb : ox;
@@ -747,9 +759,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     // the items below then need no division, no 64-bit math and no bounds arithmetic
     int *ptab = reinterpret_cast<int *>(smem) + 4 * 16 * LDT;
     for (int p = threadIdx.x; p < NPXB; p += 256) {
-        int v = -1;
-        if (p < npix) {
-            const int py = p / a.TW, px = p - (p / a.TW) * a.TW;
+        int v = -1, py, px;
+        if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
             if (oy < a.Hout && ox < a.Wout) v = ((b * a.Hout + oy) * a.Wout + ox) * a.Cout;
         }
