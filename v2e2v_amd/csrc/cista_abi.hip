@@ -1116,6 +1116,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
 extern "C" {
 
 int cista_abi_version(void) { return CISTA_ABI_VERSION; }
+#if CISTA_STAMPS
+// diagnostic builds only: the conv kernels' phase timestamps go to buf (NULL: off)
+int cista_debug_set_stamps(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(cista::g_cista_stamps), &buf, sizeof(buf)) == hipSuccess ? CISTA_OK
+                                                                                            : CISTA_ERR_HIP;
+}
+#endif
 
 const char *cista_status_string(int s) {
     switch (s) {

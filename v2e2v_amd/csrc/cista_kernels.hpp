@@ -66,10 +66,38 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_NT
 #define CISTA_NT 0
 #endif
+// taps of B fragments in flight ahead of the MFMAs in the double-buffered K loop (48-VGPR-
+// accumulator waves; the others keep 1)
+#ifndef CISTA_BPF
+#define CISTA_BPF 2
+#endif
+// VGPRs of epilogue aux inputs (x1, z, c_prev, ...) kept in flight per lane (ring of m-tiles)
+#ifndef CISTA_AUX_VGPRS
+#define CISTA_AUX_VGPRS 32
+#endif
 // Design switch (A/B builds: scripts/build_variants.sh): XCD-aware workgroup order of the conv
 // kernels (0: plain grid order; 1 measured 1 % faster per frame)
 #ifndef CISTA_XCD
 #define CISTA_XCD 1
+#endif
+// Diagnostic build only (CISTA_STAMPS=1, scripts/stamps.py): lane 0 of every conv wave records
+// shader-clock timestamps of its phases into g_cista_stamps[(block * 4 + wave) * 24 + slot]:
+// 0 hw id | xcc << 32, 1 start, 2 prologue staged, 3 + k end of K-chunk k (k < 8), 11 MFMA loop
+// done, 12 epilogue stores issued, 13/14 constant-rate (100 MHz) clock at start / end, 15
+// epilogue pixel table ready (after the workgroup barrier), 16 epilogue math done (before the
+// burst stores)
+#ifndef CISTA_STAMPS
+#define CISTA_STAMPS 0
+#endif
+#if CISTA_STAMPS
+__device__ unsigned long long *g_cista_stamps;
+#define CISTA_STAMP(slot, v)                                                                    \
+    do {                                                                                         \
+        unsigned long long *_p = g_cista_stamps;                                                 \
+        if (_p && (threadIdx.x & 63) == 0) _p[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 24 + (slot)] = (v); \
+    } while (0)
+#else
+#define CISTA_STAMP(slot, v) do { } while (0)
 #endif
 
 
@@ -464,6 +492,16 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 
     const int lane = threadIdx.x & 63;
     const int wave = threadIdx.x >> 6;
+#if CISTA_STAMPS
+    {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        CISTA_STAMP(0, (unsigned long long)hw | ((unsigned long long)xcc << 32));
+        CISTA_STAMP(13, __builtin_amdgcn_s_memrealtime());
+        CISTA_STAMP(1, __builtin_amdgcn_s_memtime());
+    }
+#endif
     const int wm = wave % WM;
     const int wn = wave / WM;
 #if CISTA_XCD
@@ -535,6 +573,9 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     };
     if constexpr (NI > 0) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
+        // B prefetch depth: deep where the accumulators leave room (the 6 x 2-tile waves)
+        constexpr int BPF_MAX = 96 / (NW * 8) - 1;          // ring <= 96 VGPRs
+        constexpr int BPF = MT_W * NW * 4 > 48 ? 1 : (CISTA_BPF < BPF_MAX ? CISTA_BPF : BPF_MAX);
         static_assert(STAGE == STAGE_S1 || STAGE == STAGE_S2 || STAGE == STAGE_ZP2 || STAGE == STAGE_CLAMP ||
                           STAGE == STAGE_S2D,
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
@@ -548,6 +589,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
             stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
         }
         __syncthreads();
+        CISTA_STAMP(2, __builtin_amdgcn_s_memtime());
         for (int kc = 0; kc < nchunks; ++kc) {
             const u32x4 *cur = smem + (kc & 1) * 8 * HPpad;
             u32x4 *nxt = smem + ((kc + 1) & 1) * 8 * HPpad;
@@ -557,51 +599,44 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
             for (int m = 0; m < MT_W; ++m) asm volatile("" : "+v"(abase[m]));
             const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
-            u32x4 bh[NW], bl[NW];
+            // B fragments D taps ahead in a ring of D + 1 slots.  vmcnt is in order, so the wait
+            // for any B load issued after the next chunk's halo loads (tap 0) also waits for the
+            // halo (an HBM round trip, ~5 us under load): with D taps loaded before them, the
+            // first such wait is at tap D + 1
+            constexpr int D = BPF;
+            u32x4 bh[D + 1][NW], bl[D + 1][NW];
 #pragma unroll
-            for (int n = 0; n < NW; ++n) {
-                bh[n] = wp[n * 128];
-                bl[n] = wp[n * 128 + 64];
-            }
+            for (int t = 0; t < D; ++t)
+#pragma unroll
+                for (int n = 0; n < NW; ++n) {
+                    bh[t][n] = wp[(size_t)t * tapstride + n * 128];
+                    bl[t][n] = wp[(size_t)t * tapstride + n * 128 + 64];
+                }
             float4 sv0[NI], sv1[NI];
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                u32x4 nh[NW], nl[NW];
-                if (tap < 8 && !CISTA_EXP_NOB) {
-                    const u32x4 *wq = wp + (size_t)(tap + 1) * tapstride;
+                if (tap + D <= 8 && !CISTA_EXP_NOB) {
+                    const u32x4 *wq = wp + (size_t)(tap + D) * tapstride;
 #pragma unroll
                     for (int n = 0; n < NW; ++n) {
-                        nh[n] = wq[n * 128];
-                        nl[n] = wq[n * 128 + 64];
-                    }
-                } else if (tap < 8) {
-#pragma unroll
-                    for (int n = 0; n < NW; ++n) {
-                        nh[n] = bh[n];
-                        nl[n] = bl[n];
+                        bh[(tap + D) % (D + 1)][n] = wq[n * 128];
+                        bl[(tap + D) % (D + 1)][n] = wq[n * 128 + 64];
                     }
                 }
-                // the next chunk's halo loads go out after B(0), B(1): the waits for those two
-                // do not include them (vmcnt is in order); they land under taps 0..1
                 if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
                     stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
 #if CISTA_PRIO == 1
                 __builtin_amdgcn_s_setprio(1);
 #endif
-                mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
+                const int slot = CISTA_EXP_NOB ? 0 : tap % (D + 1);
+                mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
 #if CISTA_PRIO == 1
                 __builtin_amdgcn_s_setprio(0);
 #endif
-                if (tap < 8) {
-#pragma unroll
-                    for (int n = 0; n < NW; ++n) {
-                        bh[n] = nh[n];
-                        bl[n] = nl[n];
-                    }
-                }
             }
             if (more && !CISTA_EXP_NOSTAGE) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg, amax);
             __syncthreads();
+            if (kc < 8) CISTA_STAMP(3 + kc, __builtin_amdgcn_s_memtime());
         }
     } else
     for (int kc = 0; kc < nchunks; ++kc) {
@@ -658,6 +693,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         }
     }
 
+    CISTA_STAMP(11, __builtin_amdgcn_s_memtime());
     // an activation beyond the fp16 range of the hi part (or inf): the result is not fp32-faithful
     if (CISTA_RANGE_CHECK && a.rflag) {
         const _Float16 m = amax[0] > amax[1] ? amax[0] : amax[1];
@@ -767,6 +803,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         ptab[p] = v;
     }
     __syncthreads();
+    CISTA_STAMP(15, __builtin_amdgcn_s_memtime());
     const int grp = lane >> 4;
     // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
     const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
@@ -801,8 +838,15 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
             if constexpr (USE_A1) A1[it] = *(const float4 *)(a.aux1 + o);
         }
     };
-    float4 curA0[NIT], curA1[NIT];
-    load_aux(0, curA0, curA1);
+    // aux ring: the aux inputs of PD m-tiles are in flight at once (issued together, then one
+    // m-tile's worth after each m-tile is consumed): under load an HBM read takes ~5 us, so a
+    // one-ahead prefetch made the epilogue a chain of MT_W round trips (scripts/stamps.py)
+    constexpr int AUXV = NIT * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
+    constexpr int PD0 = AUXV ? CISTA_AUX_VGPRS / AUXV : MT_W;
+    constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
+    float4 ringA0[PD][NIT], ringA1[PD][NIT];
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_aux(d, ringA0[d], ringA1[d]);
     // results are kept in registers (acc[m]'s registers die as res[m] is born) and stored in
     // one burst after the last aux load: no load then waits behind an outstanding store
     // the LSTC epilogues (long-K gates convs, MT_W = 12) store in the loop instead: their
@@ -812,11 +856,13 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     float4 res1[EPI == EPI_LSTM ? MT_W : 1][NIT];         // EPI_LSTM: the cell state c (out1)
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        float4 nxtA0[NIT], nxtA1[NIT];
-        // compiler-only barrier: keeps the prefetch exactly one m-tile ahead (hoisting every
-        // m-tile's loads to the top costs MT_W x NIT x 4 VGPRs and spills)
+        float4 (&curA0)[NIT] = ringA0[m % PD];
+        float4 (&curA1)[NIT] = ringA1[m % PD];
+        float4 rm[NIT];                                     // non-burst results of this m-tile
+        int om[NIT];
+        // compiler-only barrier: keeps the ring exactly PD m-tiles ahead (hoisting every m-tile's
+        // loads to the top costs MT_W x AUXV VGPRs and spills)
         asm volatile("" ::: "memory");
-        if (m + 1 < MT_W) load_aux(m + 1, nxtA0, nxtA1);
 #pragma unroll
         for (int n = 0; n < NW; ++n)
 #pragma unroll
@@ -915,25 +961,26 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                         }
                     }
                     if constexpr (BURST) res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
-#if CISTA_EXP_SMALLSTORE
-                    else if (off_raw >= 0) *(float4 *)(a.out0 + (o & (unsigned)CISTA_EXP_SMALLSTORE)) = make_float4(r[0], r[1], r[2], r[3]);
-#else
-                    else if (off_raw >= 0) *(float4 *)(a.out0 + o) = make_float4(r[0], r[1], r[2], r[3]);
-#endif
+                    else {
+                        rm[it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
+                        om[it0 / 64] = off_raw < 0 ? -1 : (int)o;
+                    }
                 }
             }
         }
-        if (m + 1 < MT_W) {
+        // this ring slot is consumed: refill it with m-tile m + PD before this m-tile's stores
+        // go out (vmcnt is in order: a load issued after a store also waits for the store)
+        if (m + PD < MT_W) load_aux(m + PD, curA0, curA1);
+        asm volatile("" ::: "memory");
+        if constexpr (!BURST)
 #pragma unroll
-            for (int it = 0; it < NIT; ++it) {
-                curA0[it] = nxtA0[it];
-                curA1[it] = nxtA1[it];
-            }
-        }
+            for (int it = 0; it < NIT; ++it)
+                if (om[it] >= 0) *(float4 *)(a.out0 + (unsigned)om[it]) = rm[it];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
         __builtin_amdgcn_wave_barrier();
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
+    CISTA_STAMP(16, __builtin_amdgcn_s_memtime());
     if constexpr (BURST)
 #pragma unroll
     for (int m = 0; m < MT_W; ++m)
@@ -956,6 +1003,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
             }
         }
+    CISTA_STAMP(12, __builtin_amdgcn_s_memtime());
+    CISTA_STAMP(14, __builtin_amdgcn_s_memrealtime());
 }
 
 // ------------------------------------------------------------------------------------------
