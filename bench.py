@@ -382,8 +382,9 @@ def time_layers(torch, model, lib_mod, vox, B, H, W, device, reps):
                              tflops=2 * macs / (ms * 1e-3) / 1e12)
         torch.cuda.synchronize()
     # the input stage computes W0 too (one composed linear map, input_w0_kernel): the W0 layer
-    # launches nothing, so its work is credited to the fused launch
-    if "W0" in res and res["W0"]["ms"] < 0.25 * res["input"]["ms"]:   # unfused: W0 ~1.3x input
+    # launches nothing (the build says so), so its work is credited to the fused launch
+    cfg = model._cfg()
+    if "W0" in res and L.cista_layer_fused(ctypes.byref(cfg), lib_mod.LAYERS.index("W0")):
         w0 = res.pop("W0")
         res["input+W0"] = dict(res.pop("input"))
         r = res["input+W0"]

@@ -178,6 +178,9 @@ enum {
 };
 /* multiply-accumulates of one launch of `layer` (per frame x B) -- the algorithmic work */
 double cista_layer_macs(const cista_config *cfg, int layer, int B, int H, int W);
+/* 1 when this build computes `layer` inside another layer's launch at inference (then
+ * cista_launch_layer(layer) launches nothing): W0 inside the composed input stage for 1..8 bins */
+int cista_layer_fused(const cista_config *cfg, int layer);
 int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, int B, int H,
                        int W, const cista_frame_io *io, void *workspace, size_t workspace_bytes,
                        void *stream);

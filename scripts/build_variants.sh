@@ -5,7 +5,7 @@
 # usage: bash scripts/build_variants.sh name1 "-DFLAG=1 ..." [name2 "-D..." ...]
 set -e
 cd "$(dirname "$0")/.."
-make -s build/cista_voxel.o build/cista_ssim.o build/cista_v2e.o
+make -s build/cista_ssim.o build/cista_v2e.o
 mkdir -p build/variants v2e2v_amd/variants
 HIPCC=${HIPCC:-/opt/rocm/bin/hipcc}
 pids=()
@@ -14,8 +14,10 @@ while [ $# -ge 2 ]; do
   (
     $HIPCC -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result $flags \
       -c -o build/variants/$name.o v2e2v_amd/csrc/cista_abi.hip &&
+    $HIPCC -O3 -std=c++17 --offload-arch=gfx950 -fPIC -Wall -Wno-unused-result $flags \
+      -c -o build/variants/${name}_vox.o v2e2v_amd/csrc/cista_voxel.hip &&
     $HIPCC --offload-arch=gfx950 -shared -o v2e2v_amd/variants/$name.so build/variants/$name.o \
-      build/cista_voxel.o build/cista_ssim.o build/cista_v2e.o && echo "built $name ($flags)"
+      build/variants/${name}_vox.o build/cista_ssim.o build/cista_v2e.o && echo "built $name ($flags)"
   ) &
   pids+=($!)
 done

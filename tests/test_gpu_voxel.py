@@ -103,6 +103,21 @@ def test_preprocess_thresholds_and_batch_shapes():
     assert torch.equal(raw.cpu(), torch.from_numpy(ref))      # not modified
 
 
+@pytest.mark.parametrize("H,W,sizes", [(64, 64, [40000, 16384, 16385, 3]), (180, 240, [33000, 15000])])
+def test_multi_segment_windows(H, W, sizes):
+    """Windows larger than one sorted segment of the fused per-window kernel (16384 events):
+    their left contributions of every segment go first, then the right ones, in event order."""
+    rng = np.random.default_rng(sum(sizes))
+    nb = 5
+    wins = _windows(rng, H, W, sizes, hot=True)
+    got = ep.events_to_voxel_batch(wins, nb, W, H).cpu().numpy()
+    for b, ev in enumerate(wins):
+        assert_bits(got[b], ref_raw(ev, nb, W, H))
+    got = ep.events_to_voxel_batch(wins, nb, W, H, mode="std", filter_hot_pixel=True).cpu().numpy()
+    for b, ev in enumerate(wins):
+        assert_bits(got[b], fx.normalize_voxel(ref_raw(ev, nb, W, H), True, "std"))
+
+
 def test_large_frame_many_events():
     """720x1280 (the V2E2V resolution, config c5): 563 reduction chunks per window."""
     rng = np.random.default_rng(11)

@@ -36,6 +36,11 @@ def test_sizes_and_invalid_config():
     io = _lib.CistaFrameIO()
     st = L.cista_forward(ctypes.byref(cfg), None, 1, 64, 64, ctypes.byref(io), None, 0, None)
     assert st == 1
+    # W0 is computed inside the composed input stage for 1..8 bins (bench.py asks the build)
+    W0, IN = _lib.LAYERS.index("W0"), _lib.LAYERS.index("input")
+    assert L.cista_layer_fused(ctypes.byref(cfg), W0) == 1
+    assert L.cista_layer_fused(ctypes.byref(cfg), IN) == 0
+    assert L.cista_layer_fused(ctypes.byref(_lib.CistaConfig(64, 5, 9)), W0) == 0
     odd = _lib.CistaConfig(48, 5, 5)   # base_channels % 32 != 0 -> unsupported, not wrong
     assert L.cista_forward(ctypes.byref(odd), ctypes.c_void_p(1), 1, 64, 64,
                            ctypes.byref(io), None, 0, None) == 2

@@ -1368,6 +1368,11 @@ double cista_layer_macs(const cista_config *cfg, int layer, int B, int H, int W)
     return layer_macs(*cfg, layer, B, H, W);
 }
 
+int cista_layer_fused(const cista_config *cfg, int layer) {
+    if (!cfg_ok(cfg)) return 0;
+    return layer == CISTA_LAYER_W0 && fused_input(*cfg) ? 1 : 0;
+}
+
 int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, int B, int H, int W,
                        const cista_frame_io *io, void *workspace, size_t workspace_bytes,
                        void *stream) {

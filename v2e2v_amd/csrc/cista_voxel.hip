@@ -19,11 +19,21 @@
 
 #include <hip/hip_runtime.h>
 #include <hipcub/hipcub.hpp>
+#include <mutex>
 
 #include "../../include/cista_lstc.h"
 #include "../../include/cista_voxel.h"
 
 namespace cista_vox {
+
+// timing-only switch (results WRONG when set): 1 skip the group walk, 2 skip the block sort,
+// 3 skip the grid zeroing
+#ifndef CISTA_VOX_EXP
+#define CISTA_VOX_EXP 0
+#endif
+#ifndef CISTA_VOX_FUSED
+#define CISTA_VOX_FUSED 1   // 0: keys + global radix sort + accum for every grid size (A/B builds)
+#endif
 
 constexpr int CHUNK = 8192;    // numpy ufunc buffer size: the float32 reduction runs per chunk
 constexpr int LEAF = 128;      // numpy pairwise-sum block (PW_BLOCKSIZE)
@@ -149,6 +159,303 @@ __global__ void vox_accum_kernel(const unsigned long long *keys, const int *vals
     }
 }
 
+// ------------------------------------------------------------------------------------------
+// Per-window sort + tiled accumulation (replaces keys + global radix sort + memset + accum when
+// the grid has < 2^18 pixels and num_bins <= WNB):
+//   vox_sort_kernel (one 512-thread workgroup per window): the window's events in segments of
+//     WSEG, key = pixel << 14 | event-in-segment (unique: the sort needs no stability; events
+//     outside the grid get a sentinel that sorts last), block radix sort in LDS, sorted keys to
+//     the workspace; for single-segment windows also the first sorted position of every tile;
+//   vox_tile_kernel (one workgroup per (tile of TP pixels x num_bins bins, window)): zero the
+//     tile in LDS, walk the pixel groups of the tile (contiguous in the sorted keys) -- one
+//     thread per group, left contributions first, then right ones, in event order: the
+//     reference's per-voxel order -- and write the tile out densely (zeros included: no memset).
+// Windows of more than one segment walk every segment's range of the tile, left passes of all
+// segments first, then right passes, barriers in between.
+// ------------------------------------------------------------------------------------------
+constexpr int WT = 512;                    // threads of the sort kernel
+constexpr int WITEMS = 32;                 // sort items per thread
+constexpr int WSEG = WT * WITEMS;          // events per sorted segment (14-bit local index)
+constexpr int WNB = 8;                     // bins held in registers by a group walk
+constexpr int TT = 256;                    // threads of the tile kernel
+constexpr int WTILE = 12288;               // floats of a tile (TP = WTILE / num_bins pixels)
+constexpr int TBMAX = 256;                 // tiles per window (TP >= 1536 and HW < 2^18: <= 171)
+typedef hipcub::BlockRadixSort<unsigned, WT, WITEMS> WinSort;
+typedef hipcub::BlockExchange<unsigned, WT, WITEMS> WinExch;
+struct WinLds {
+    union {
+        typename WinSort::TempStorage sort;
+        typename WinExch::TempStorage exch;
+        unsigned keys[WSEG];               // the sorted segment
+    } u;
+};
+
+__host__ __device__ inline int tile_pixels(int nb) { return (WTILE / nb) & ~3; }
+
+// first sorted position in [0, n) whose pixel (key >> 14) is >= p
+__device__ __forceinline__ int key_lower(const unsigned *k, int n, unsigned p) {
+    int lo = 0, hi = n;
+    const unsigned kk = p << 14;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (k[mid] < kk) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+}
+
+// grid (B), block WT, dynamic LDS sizeof(WinLds).  scratch: n_events sorted keys (window b's
+// segments at its event offsets); tb: TBMAX + 1 tile starts per window (single-segment windows)
+__global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const long long *off, int nb, int H, int W,
+                                                      int end_bit, unsigned *scratch, double2 *tp_sorted, int *tb) {
+    extern __shared__ __align__(16) char wsm[];
+    WinLds &L = *reinterpret_cast<WinLds *>(wsm);
+    const int b = blockIdx.x, tid = threadIdx.x;
+    const long long e0 = off[b];
+    const int n = (int)(off[b + 1] - e0);
+    const int nseg = (n + WSEG - 1) / WSEG;
+    for (int sg = 0; sg < nseg; ++sg) {
+        const long long base = e0 + (long long)sg * WSEG;
+        const int cnt = min(WSEG, n - sg * WSEG);
+        unsigned key[WITEMS];
+        // striped (coalesced) rows, loads issued branch-free in batches (a load under a branch is
+        // waited for before the branch joins: 32 serial HBM round trips per thread)
+        constexpr int LB = 8;
+#pragma unroll
+        for (int i0 = 0; i0 < WITEMS; i0 += LB) {
+            double x[LB], y[LB];
+#pragma unroll
+            for (int i = 0; i < LB; ++i) {
+                const int l = min((i0 + i) * WT + tid, cnt - 1);
+                const double2 r = *reinterpret_cast<const double2 *>(ev + 4 * (base + l) + 1);
+                x[i] = r.x;
+                y[i] = r.y;
+            }
+#pragma unroll
+            for (int i = 0; i < LB; ++i) {
+                const int l = (i0 + i) * WT + tid;
+                // reference :42-43: astype(np.uint) truncates toward zero
+                const bool in = l < cnt && x[i] > -1.0 && x[i] < (double)W && y[i] > -1.0 && y[i] < (double)H;
+                key[i0 + i] = in ? ((((unsigned)y[i] * (unsigned)W + (unsigned)x[i]) << 14) | (unsigned)l) : 0xFFFFFFFFu;
+            }
+        }
+        __syncthreads();                                                // LDS union reuse
+        WinExch(L.u.exch).StripedToBlocked(key, key);
+        __syncthreads();
+        if (CISTA_VOX_EXP != 2) WinSort(L.u.sort).SortBlockedToStriped(key, 0, end_bit);
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < WITEMS; ++i) {
+            const int l = i * WT + tid;
+            if (nseg == 1) L.u.keys[l] = key[i];
+            if (l < cnt) scratch[base + l] = key[i];
+        }
+        // (t, polarity) of every event in sorted order: the rows were read just above (L2 /
+        // Infinity Cache), the tile kernel then streams them instead of gathering from HBM
+#pragma unroll
+        for (int i0 = 0; i0 < WITEMS; i0 += 8) {
+            double2 r[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int l = min((i0 + i) * WT + tid, cnt - 1);
+                const unsigned kk = key[i0 + i];
+                const double *e = ev + 4 * (base + (kk == 0xFFFFFFFFu ? l : (long long)(kk & 0x3FFF)));
+                r[i] = make_double2(e[0], e[3]);
+            }
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int l = (i0 + i) * WT + tid;
+                if (l < cnt) tp_sorted[base + l] = r[i];
+            }
+        }
+    }
+    if (nseg == 1) {
+        __syncthreads();
+        const unsigned HW = (unsigned)H * (unsigned)W;
+        const int TP = tile_pixels(nb);
+        const int ntiles = (int)((HW + TP - 1) / TP);
+        for (int t = tid; t <= ntiles; t += WT) tb[(size_t)b * (TBMAX + 1) + t] = key_lower(L.u.keys, n, min((unsigned)t * TP, HW));
+    }
+}
+
+// ---- group walks of the tile kernel; cell (bin, pixel p) = tile[bin * TP + p - pa] ----
+// General walk (RMW on the LDS cells): sorted positions [s, e) of one segment; pass 1 = left
+// contributions, 2 = right, 3 = both (in that order: single-segment windows)
+template <bool TORCH>
+__device__ void walk_groups(const unsigned *k, int s, int e, const double2 *tps, double first, double dT, int nb,
+                            float *tile, int TP, unsigned pa, int pass) {
+    for (int j = s + (int)threadIdx.x; j < e; j += TT) {
+        const unsigned p = k[j] >> 14;
+        if (j > s && (k[j - 1] >> 14) == p) continue;                   // not the group head
+        int g = j;
+        while (g < e && (k[g] >> 14) == p) ++g;                         // group [j, g)
+        float *cell = tile + (p - pa);
+        for (int ph = 1; ph <= 2; ++ph) {
+            if (!(pass & ph)) continue;
+            for (int q = j; q < g; ++q) {
+                const double2 r = tps[q];
+                const double ev[4] = {r.x, 0.0, 0.0, r.y};
+                if (TORCH) {
+                    EvValT v;
+                    if (!event_value_torch(ev, first, dT, nb, v)) continue;
+                    const unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    if (bin < (unsigned long long)nb) cell[bin * TP] += ph == 1 ? v.vl : v.vr;
+                } else {
+                    EvVal v;
+                    if (!event_value(ev, first, dT, nb, v)) continue;
+                    const unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    if (bin < (unsigned long long)nb) {
+                        float *d = cell + bin * TP;
+                        *d = (float)((double)*d + (ph == 1 ? v.vl : v.vr));
+                    }
+                }
+            }
+        }
+    }
+}
+
+// Fast walk (single-segment windows, nb <= WNB): a group's nb cells start at zero and only its
+// thread touches them, so they are accumulated in registers -- the same adds in the same order
+// -- and only the touched cells are stored; a lone event (most pixels) is evaluated once.  The
+// thread's positions are taken WB at a time and their event rows gathered up front.
+#ifndef CISTA_VOX_WB
+#define CISTA_VOX_WB 4
+#endif
+constexpr int WB = CISTA_VOX_WB;
+template <bool TORCH>
+__device__ void walk_fast(const unsigned *k, int s, int e, const double2 *tps, double first, double dT, int nb,
+                          float *tile, int TP, unsigned pa) {
+    for (int j0 = s + (int)threadIdx.x; j0 < e; j0 += WB * TT) {
+        unsigned kp[WB];
+        double t[WB], pl[WB];
+#pragma unroll
+        for (int u = 0; u < WB; ++u) {                                  // branch-free gathers
+            const int j = min(j0 + u * TT, e - 1);
+            kp[u] = k[j];
+            const double2 r = tps[j];
+            t[u] = r.x;
+            pl[u] = r.y;
+        }
+#pragma unroll
+        for (int u = 0; u < WB; ++u) {
+            const int j = j0 + u * TT;
+            if (j >= e) break;
+            const unsigned p = kp[u] >> 14;
+            if (j > s && (k[j - 1] >> 14) == p) continue;               // not the group head
+            float *cell = tile + (p - pa);
+            const bool lone = j + 1 == e || (k[j + 1] >> 14) != p;
+            if (lone) {             // the only left and the only right contribution of two cells
+                double e4[4];
+                e4[0] = t[u];
+                e4[3] = pl[u];
+                if (TORCH) {
+                    EvValT v;
+                    if (!event_value_torch(e4, first, dT, nb, v)) continue;
+                    if (v.ti < (unsigned long long)nb) cell[v.ti * TP] = 0.0f + v.vl;
+                    if (v.ti + 1 < (unsigned long long)nb) cell[(v.ti + 1) * TP] = 0.0f + v.vr;
+                } else {
+                    EvVal v;
+                    if (!event_value(e4, first, dT, nb, v)) continue;
+                    if (v.ti < (unsigned long long)nb) cell[v.ti * TP] = (float)(0.0 + v.vl);
+                    if (v.ti + 1 < (unsigned long long)nb) cell[(v.ti + 1) * TP] = (float)(0.0 + v.vr);
+                }
+                continue;
+            }
+            int g = j + 1;
+            while (g < e && (k[g] >> 14) == p) ++g;                     // group [j, g)
+            float acc[WNB];
+#pragma unroll
+            for (int bb = 0; bb < WNB; ++bb) acc[bb] = 0.0f;
+            unsigned touched = 0;
+            for (int ph = 1; ph <= 2; ++ph)                             // left, then right
+                for (int q = j; q < g; ++q) {
+                    const double2 rr = tps[q];
+                    const double r[4] = {rr.x, 0.0, 0.0, rr.y};
+                    unsigned long long bin;
+                    double vd = 0.0;
+                    float vf = 0.0f;
+                    if (TORCH) {
+                        EvValT v;
+                        if (!event_value_torch(r, first, dT, nb, v)) continue;
+                        bin = v.ti + (ph == 2 ? 1 : 0);
+                        vf = ph == 1 ? v.vl : v.vr;
+                    } else {
+                        EvVal v;
+                        if (!event_value(r, first, dT, nb, v)) continue;
+                        bin = v.ti + (ph == 2 ? 1 : 0);
+                        vd = ph == 1 ? v.vl : v.vr;
+                    }
+                    if (bin >= (unsigned long long)nb) continue;
+#pragma unroll
+                    for (int bb = 0; bb < WNB; ++bb)
+                        if ((unsigned long long)bb == bin) acc[bb] = TORCH ? acc[bb] + vf : (float)((double)acc[bb] + vd);
+                    touched |= 1u << bin;
+                }
+#pragma unroll
+            for (int bb = 0; bb < WNB; ++bb)
+                if (touched & (1u << bb)) cell[bb * TP] = acc[bb];
+        }
+    }
+}
+
+// grid (ntiles, B), block TT
+template <bool TORCH>
+__global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const long long *off, int nb, int H, int W,
+                                                      const unsigned *scratch, const double2 *tps, const int *tb,
+                                                      float *vox) {
+    __shared__ __align__(16) float tile[WTILE];
+    __shared__ int rng[2];
+    const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
+    const long long e0 = off[b];
+    const int n = (int)(off[b + 1] - e0);
+    const int nseg = (n + WSEG - 1) / WSEG;
+    const unsigned HW = (unsigned)H * (unsigned)W;
+    const int TP = tile_pixels(nb);
+    const unsigned pa = (unsigned)t * TP;
+    const int np = (int)min((unsigned)TP, HW - pa);
+    double first = 0.0, dT = 1.0;
+    if (n > 0) {
+        first = ev[4 * e0];
+        dT = ev[4 * (e0 + n - 1)] - first;                              // :37-38
+        if (dT == 0.0) dT = 1.0;                                        // :40-41
+    }
+    for (int i = tid; i < nb * TP; i += TT) tile[i] = 0.0f;
+    __syncthreads();
+    if (CISTA_VOX_EXP == 1) {
+    } else if (nseg == 1) {
+        const int *tbw = tb + (size_t)b * (TBMAX + 1);
+        const int s = tbw[t], e = tbw[t + 1];
+        if (nb <= WNB) walk_fast<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa);
+        else walk_groups<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa, 3);
+    } else if (nseg > 1) {
+        for (int pass = 1; pass <= 2; ++pass)                            // np.add.at #1, then #2
+            for (int sg = 0; sg < nseg; ++sg) {
+                const long long base = e0 + (long long)sg * WSEG;
+                const int cnt = min(WSEG, n - sg * WSEG);
+                if (tid == 0) {
+                    rng[0] = key_lower(scratch + base, cnt, pa);
+                    rng[1] = key_lower(scratch + base, cnt, pa + np);
+                }
+                __syncthreads();
+                walk_groups<TORCH>(scratch + base, rng[0], rng[1], tps + base, first, dT, nb, tile, TP, pa, pass);
+                __syncthreads();
+            }
+    }
+    __syncthreads();
+    float *out = vox + (size_t)b * nb * HW + pa;
+    const bool vec = (((size_t)out) & 15) == 0 && (HW & 3) == 0;
+    for (int kb = 0; kb < nb; ++kb) {                                    // dense rows, zeros included
+        float *row = out + (size_t)kb * HW;
+        const float *src = tile + kb * TP;
+        if (vec) {
+            for (int i = tid; i < np / 4; i += TT)
+                reinterpret_cast<float4 *>(row)[i] = reinterpret_cast<const float4 *>(src)[i];
+            for (int i = (np & ~3) + tid; i < np; i += TT) row[i] = src[i];
+        } else {
+            for (int i = tid; i < np; i += TT) row[i] = src[i];
+        }
+    }
+}
+
 __device__ __forceinline__ float hot(float v, float thr) { return (thr > 0.0f && fabsf(v) > thr) ? 0.0f : v; }
 
 __device__ __forceinline__ int pw_split(int n) {
@@ -244,28 +551,76 @@ __global__ __launch_bounds__(MAX_LEAVES) void vox_chunk_kernel(const float *vox,
     // coalesced staging + count / min / max (order-independent)
     int cnt = 0;
     float mn = INFINITY, mx = -INFINITY;
-    constexpr int U = 8;
-    for (int i0 = tid; i0 < m; i0 += U * MAX_LEAVES) {
-        float v[U];
+    if (full && (((size_t)a) & 15) == 0) {
+        // float4 loads: 4 consecutive elements always lie in one leaf row of the LDS image
+        constexpr int U4 = CHUNK / 4 / MAX_LEAVES;                   // 16 float4 per thread
+        float4 v[U4];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * MAX_LEAVES;
-            v[u] = i < m ? hot(a[i], thr) : 0.0f;
+        for (int u = 0; u < U4; ++u) v[u] = reinterpret_cast<const float4 *>(a)[tid + u * MAX_LEAVES];
+#pragma unroll
+        for (int u = 0; u < U4; ++u) {
+            const int i = (tid + u * MAX_LEAVES) * 4;
+            const float e[4] = {hot(v[u].x, thr), hot(v[u].y, thr), hot(v[u].z, thr), hot(v[u].w, thr)};
+            float *dst = buf + (i >> 7) * LSTRIDE + (i & 127);
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                dst[k] = e[k];
+                cnt += e[k] != 0.0f;
+                mn = fminf(mn, e[k]);
+                mx = fmaxf(mx, e[k]);
+            }
         }
+    } else {
+        constexpr int U = 8;
+        for (int i0 = tid; i0 < m; i0 += U * MAX_LEAVES) {
+            float v[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int i = i0 + u * MAX_LEAVES;
-            if (i < m) {
-                buf[(i >> 7) * LSTRIDE + (i & 127)] = v[u];
-                cnt += v[u] != 0.0f;
-                mn = fminf(mn, v[u]);
-                mx = fmaxf(mx, v[u]);
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * MAX_LEAVES;
+                v[u] = i < m ? hot(a[i], thr) : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int i = i0 + u * MAX_LEAVES;
+                if (i < m) {
+                    buf[(i >> 7) * LSTRIDE + (i & 127)] = v[u];
+                    cnt += v[u] != 0.0f;
+                    mn = fminf(mn, v[u]);
+                    mx = fmaxf(mx, v[u]);
+                }
             }
         }
     }
     rcnt[tid] = cnt; rmn[tid] = mn; rmx[tid] = mx;
     __syncthreads();
-    if (tid < nleaves) leaf_sums_lds(buf, lstart[tid], llen[tid], ls[tid], lq[tid]);
+    if (full) {
+        // the 64 full leaves' 8 accumulator chains (numpy's unrolled leaf: r[c] = v[c], then
+        // r[c] += v[c + 8i]) spread over all 128 threads: thread (o, l) runs chains 4o..4o+3 of
+        // leaf l and forms ((r[4o] + r[4o+1]) + (r[4o+2] + r[4o+3])); the leaf sum is the o = 0
+        // half + the o = 1 half, exactly numpy's association
+        const int l = tid & 63, o = tid >> 6;
+        const float *row = buf + l * LSTRIDE + 4 * o;
+        float r[4], rq[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            r[k] = row[k];
+            rq[k] = r[k] * r[k];
+        }
+#pragma unroll
+        for (int i = 1; i < LEAF / 8; ++i)
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                const float v = row[8 * i + k];
+                r[k] += v;
+                rq[k] += v * v;
+            }
+        const float hs = (r[0] + r[1]) + (r[2] + r[3]), hq = (rq[0] + rq[1]) + (rq[2] + rq[3]);
+        if (o == 1) { ls[l] = hs; lq[l] = hq; }
+        __syncthreads();
+        if (o == 0) { ls[l] = hs + ls[l]; lq[l] = hq + lq[l]; }
+    } else if (tid < nleaves) {
+        leaf_sums_lds(buf, lstart[tid], llen[tid], ls[tid], lq[tid]);
+    }
     for (int k = MAX_LEAVES / 2; k > 0; k >>= 1) {
         if (tid < k) {
             rcnt[tid] += rcnt[tid + k];
@@ -367,29 +722,44 @@ __global__ void vox_stats_kernel(const ChunkPart *parts, int nchunks, int B, int
     st[b] = w;
 }
 
-__global__ void vox_apply_kernel(float *vox, long long n, int B, int mode, float thr, const WinStats *st) {
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n * B) return;
-    const int b = (int)(i / n);
-    const float v = hot(vox[i], thr);                        // :137-138
+__device__ __forceinline__ float apply1(float v0, int mode, float thr, const WinStats &w) {
+    const float v = hot(v0, thr);                            // :137-138
     float r = v;
     if (mode == CISTA_VOXEL_STD) {
-        const WinStats w = st[b];
         if (w.nnz > 0) {                                     // :146
             const double mask = v != 0.0f ? 1.0 : 0.0;
             r = (float)(mask * ((double)v - w.mean) / (w.std + 1e-8));   // :152
         }
     } else if (mode == CISTA_VOXEL_STD_F32) {
-        const WinStats w = st[b];
         if (w.nnz > 0) {                                     // :170, float32: mask * (v - mean) / (std + 1e-8)
             const float mask = v != 0.0f ? 1.0f : 0.0f;
             r = mask * (v - (float)w.mean) / ((float)w.std + 1e-8f);
         }
     } else if (mode == CISTA_VOXEL_MAXMIN) {
-        const WinStats w = st[b];
         r = (v - w.mn) / (w.mx - w.mn + 1e-8f);              // :140
     }
-    vox[i] = r;
+    return r;
+}
+
+// grid (ceil(n / 1024), B), block 256: 4 consecutive elements of window blockIdx.y per thread,
+// as one float4 when the window's grid is 16-byte aligned
+__global__ void vox_apply_kernel(float *vox, long long n, int mode, float thr, const WinStats *st) {
+    const int b = blockIdx.y;
+    const long long i = ((long long)blockIdx.x * blockDim.x + threadIdx.x) * 4;
+    if (i >= n) return;
+    WinStats w;
+    if (mode != CISTA_VOXEL_RAW) w = st[b];
+    float *g = vox + (size_t)b * n + i;
+    if (i + 4 <= n && (((size_t)g) & 15) == 0) {
+        float4 v = *reinterpret_cast<float4 *>(g);
+        v.x = apply1(v.x, mode, thr, w);
+        v.y = apply1(v.y, mode, thr, w);
+        v.z = apply1(v.z, mode, thr, w);
+        v.w = apply1(v.w, mode, thr, w);
+        *reinterpret_cast<float4 *>(g) = v;
+    } else {
+        for (long long k = 0; k < 4 && i + k < n; ++k) g[k] = apply1(g[k], mode, thr, w);
+    }
 }
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -397,6 +767,8 @@ inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 struct VoxWs {
     unsigned long long *k0, *k1;
     int *v0, *v1;
+    int *tb;                 // per-window tile starts of the sort + tile path
+    void *tps;               // (t, polarity) of every event in sorted order (same path)
     ChunkPart *parts;
     WinStats *stats;
     void *cub;
@@ -425,6 +797,8 @@ VoxWs carve(void *base, int B, long long N, int nb, int H, int W) {
     w.k1 = static_cast<unsigned long long *>(take(NN * 8));
     w.v0 = static_cast<int *>(take(NN * 4));
     w.v1 = static_cast<int *>(take(NN * 4));
+    w.tb = static_cast<int *>(take((size_t)(B > 0 ? B : 1) * (TBMAX + 1) * 4));
+    w.tps = take(NN * 16);
     w.parts = static_cast<ChunkPart *>(take((size_t)(B > 0 ? B : 1) * nchunks * sizeof(ChunkPart)));
     w.stats = static_cast<WinStats *>(take((size_t)(B > 0 ? B : 1) * sizeof(WinStats)));
     w.cub_bytes = 0;
@@ -441,6 +815,20 @@ VoxWs carve(void *base, int B, long long N, int nb, int H, int W) {
 
 inline dim3 g1d(long long n, int bs = 256) { return dim3((unsigned)((n + bs - 1) / bs)); }
 
+// dynamic LDS above 64 KiB is enabled per kernel, once (thread-safe)
+bool big_lds(const void *kern) {
+    static std::mutex mu;
+    static const void *done[4];
+    static int ndone = 0;
+    std::lock_guard<std::mutex> lock(mu);
+    for (int i = 0; i < ndone; ++i)
+        if (done[i] == kern) return true;
+    if (hipFuncSetAttribute(kern, hipFuncAttributeMaxDynamicSharedMemorySize, (int)sizeof(WinLds)) != hipSuccess)
+        return false;
+    if (ndone < 4) done[ndone++] = kern;
+    return true;
+}
+
 // hot-pixel filter + normalisation of B grids of n floats, in place
 int preprocess(float *voxels, int B, long long n, int mode, float thr, const VoxWs &w, hipStream_t st) {
     const int nchunks = (int)((n + CHUNK - 1) / CHUNK);
@@ -451,8 +839,9 @@ int preprocess(float *voxels, int B, long long n, int mode, float thr, const Vox
                            mode, w.stats);
     }
     if (mode != CISTA_VOXEL_RAW || thr > 0.0f)
-        hipLaunchKernelGGL(vox_apply_kernel, g1d(n * B), dim3(256), 0, st, voxels, n, B, mode, thr,
-                           (const WinStats *)w.stats);
+        for (int b0 = 0; b0 < B; b0 += 65535)                 // grid.y <= 65535 windows per launch
+            hipLaunchKernelGGL(vox_apply_kernel, dim3((unsigned)((n + 1023) / 1024), min(B - b0, 65535)), dim3(256),
+                               0, st, voxels + (size_t)b0 * n, n, mode, thr, (const WinStats *)w.stats + b0);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
 
@@ -481,6 +870,23 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
     if (workspace_bytes < w.bytes) return CISTA_ERR_WORKSPACE;
     hipStream_t st = static_cast<hipStream_t>(stream);
     const long long n = (long long)num_bins * height * width;
+    const unsigned long long HW = (unsigned long long)height * width;
+    const long long tp = num_bins * 4 <= WTILE ? tile_pixels(num_bins) : 0;
+    if (CISTA_VOX_FUSED && HW < (1ull << 18) - 1 && tp > 0 && ((long long)HW + tp - 1) / tp <= TBMAX) {
+        // per-window sort + tiled accumulation (no memset, no global sort)
+        if (!big_lds(reinterpret_cast<const void *>(vox_sort_kernel))) return CISTA_ERR_HIP;
+        const int ntiles = (int)(((long long)HW + tp - 1) / tp);
+        unsigned *scr = reinterpret_cast<unsigned *>(w.k0);
+        int *tb = reinterpret_cast<int *>(w.tb);
+        double2 *tps = reinterpret_cast<double2 *>(w.tps);
+        hipLaunchKernelGGL(vox_sort_kernel, dim3(B), dim3(WT), sizeof(WinLds), st, events, offsets, num_bins, height,
+                           width, 14 + end_bits(HW), scr, tps, tb);
+        hipLaunchKernelGGL(torch_acc ? vox_tile_kernel<true> : vox_tile_kernel<false>, dim3(ntiles, B), dim3(TT), 0,
+                           st, events, offsets, num_bins, height, width, (const unsigned *)scr, (const double2 *)tps,
+                           (const int *)tb, voxels);
+        if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
+        return preprocess(voxels, B, n, mode, hot_threshold, w, st);
+    }
     if (hipMemsetAsync(voxels, 0, (size_t)B * n * sizeof(float), st) != hipSuccess) return CISTA_ERR_HIP;
     if (n_events > 0) {
         hipLaunchKernelGGL(vox_keys_kernel, g1d(n_events), dim3(256), 0, st, events, offsets, B, n_events, height,
