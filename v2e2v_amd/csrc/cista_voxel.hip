@@ -243,29 +243,32 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
         __syncthreads();
         if (CISTA_VOX_EXP != 2) WinSort(L.u.sort).SortBlockedToStriped(key, 0, end_bit);
         __syncthreads();
+        // (t, polarity) of every event in sorted order, for the tile kernel to stream: the rows
+        // are re-read in event order (coalesced, L2 / Infinity-Cache hot) in rounds of WPR
+        // events, staged in LDS (the sort storage) and picked up by the sorted positions
+        constexpr int WPR = 4096;
+        double2 *pay = reinterpret_cast<double2 *>(&L.u);
+        static_assert(WPR * sizeof(double2) <= sizeof(L.u), "payload round fits the sort storage");
+        for (int r0 = 0; r0 < cnt; r0 += WPR) {
+            __syncthreads();
+            for (int l = r0 + tid; l < min(cnt, r0 + WPR); l += WT) {
+                const double *e = ev + 4 * (base + l);
+                pay[l - r0] = make_double2(e[0], e[3]);
+            }
+            __syncthreads();
+#pragma unroll
+            for (int i = 0; i < WITEMS; ++i) {
+                const int l = i * WT + tid;
+                const int idx = (int)(key[i] & 0x3FFF);
+                if (l < cnt && key[i] != 0xFFFFFFFFu && idx >= r0 && idx < r0 + WPR) tp_sorted[base + l] = pay[idx - r0];
+            }
+        }
+        __syncthreads();
 #pragma unroll
         for (int i = 0; i < WITEMS; ++i) {
             const int l = i * WT + tid;
             if (nseg == 1) L.u.keys[l] = key[i];
             if (l < cnt) scratch[base + l] = key[i];
-        }
-        // (t, polarity) of every event in sorted order: the rows were read just above (L2 /
-        // Infinity Cache), the tile kernel then streams them instead of gathering from HBM
-#pragma unroll
-        for (int i0 = 0; i0 < WITEMS; i0 += 8) {
-            double2 r[8];
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int l = min((i0 + i) * WT + tid, cnt - 1);
-                const unsigned kk = key[i0 + i];
-                const double *e = ev + 4 * (base + (kk == 0xFFFFFFFFu ? l : (long long)(kk & 0x3FFF)));
-                r[i] = make_double2(e[0], e[3]);
-            }
-#pragma unroll
-            for (int i = 0; i < 8; ++i) {
-                const int l = (i0 + i) * WT + tid;
-                if (l < cnt) tp_sorted[base + l] = r[i];
-            }
         }
     }
     if (nseg == 1) {
@@ -322,9 +325,10 @@ __device__ void walk_groups(const unsigned *k, int s, int e, const double2 *tps,
 #endif
 constexpr int WB = CISTA_VOX_WB;
 template <bool TORCH>
-__device__ void walk_fast(const unsigned *k, int s, int e, const double2 *tps, double first, double dT, int nb,
+__device__ void walk_fast(const unsigned *k, int e, const double2 *tps, double first, double dT, int nb,
                           float *tile, int TP, unsigned pa) {
-    for (int j0 = s + (int)threadIdx.x; j0 < e; j0 += WB * TT) {
+    // positions [0, e) of the tile: k[j] its sorted keys, tps[j] their (t, polarity)
+    for (int j0 = (int)threadIdx.x; j0 < e; j0 += WB * TT) {
         unsigned kp[WB];
         double t[WB], pl[WB];
 #pragma unroll
@@ -340,7 +344,7 @@ __device__ void walk_fast(const unsigned *k, int s, int e, const double2 *tps, d
             const int j = j0 + u * TT;
             if (j >= e) break;
             const unsigned p = kp[u] >> 14;
-            if (j > s && (k[j - 1] >> 14) == p) continue;               // not the group head
+            if (j > 0 && (k[j - 1] >> 14) == p) continue;               // not the group head
             float *cell = tile + (p - pa);
             const bool lone = j + 1 == e || (k[j + 1] >> 14) != p;
             if (lone) {             // the only left and the only right contribution of two cells
@@ -424,8 +428,11 @@ __global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const lo
     } else if (nseg == 1) {
         const int *tbw = tb + (size_t)b * (TBMAX + 1);
         const int s = tbw[t], e = tbw[t + 1];
-        if (nb <= WNB) walk_fast<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa);
-        else walk_groups<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa, 3);
+        if (nb <= WNB) {
+            walk_fast<TORCH>(scratch + e0 + s, e - s, tps + e0 + s, first, dT, nb, tile, TP, pa);
+        } else {
+            walk_groups<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa, 3);
+        }
     } else if (nseg > 1) {
         for (int pass = 1; pass <= 2; ++pass)                            // np.add.at #1, then #2
             for (int sg = 0; sg < nseg; ++sg) {
