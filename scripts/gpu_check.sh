@@ -17,7 +17,7 @@ for step in "$@"; do
       rc=$?; echo "bench rc=$rc"; cat gpurun_out/bench.json; tail -3 gpurun_out/bench.err; [ $rc -eq 0 ] || exit $rc ;;
     prof)
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
-      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/prof -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --sweep "" > gpurun_out/prof_bench.json 2> gpurun_out/prof.err
       rc=$?; echo "prof rc=$rc"; tail -3 gpurun_out/prof.err; [ $rc -eq 0 ] || exit $rc ;;
     ttests)
       timeout -k 10 600 python -m pytest tests/test_gpu_train.py -m gpu -q -p no:cacheprovider > gpurun_out/gpu_ttests.log 2>&1
@@ -32,6 +32,10 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/proft -o run -- python3 bench.py --mode train --steps 1 --warmup 1 > gpurun_out/proft_bench.json 2> gpurun_out/proft.err
       rc=$?; echo "tprof rc=$rc"; tail -3 gpurun_out/proft.err; [ $rc -eq 0 ] || exit $rc ;;
+    vprof)
+      cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
+      timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profv -o run -- python3 bench.py --mode v2e2v --steps 1 --warmup 1 > gpurun_out/profv_bench.json 2> gpurun_out/profv.err
+      rc=$?; echo "vprof rc=$rc"; tail -3 gpurun_out/profv.err; [ $rc -eq 0 ] || exit $rc ;;
     vtests)
       # persistent-loop parity of every variant build (bit-exact batch vs single runs)
       for f in v2e2v_amd/variants/*.so; do

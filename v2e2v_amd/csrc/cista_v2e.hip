@@ -78,10 +78,12 @@ struct State {   // device planes, B*H*W each
     float *base, *lp, *pos, *neg, *pos_pre, *neg_pre, *noise_rate, *tmem;
 };
 
+constexpr int MAXSLOTS = 64;    // atomic slots per batch element of the image max
+
 struct Scratch {
     int *counts;          // B*H*W event counts of the current frame
     float *pol;           // B*H*W polarity (+1 / -1 / 0)
-    int *iters_raw;       // [B] image max of counts
+    int *iters_raw;       // [B][MAXSLOTS] image max of counts (partial maxima)
     int *num_iters;       // [B] max(iters_raw, 1)
     float *ts_step;       // [B]
     int *meta;            // [0] max_num_iters, [1] refractory switch
@@ -171,15 +173,31 @@ __global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch 
         w.counts[i] = cnt;
         w.pol[i] = pol;
     }
-    // image max of the counts per batch element: wave max, then one atomic per wave (exact)
+    // image max of the counts per batch element (exact in any order): wave max, workgroup max
+    // in LDS, then one atomic per workgroup into one of MAXSLOTS slots of the element (thousands
+    // of workgroups on one address serialise: ~10 ns each, 145 us per 720x1280 frame)
+    __shared__ int wmax[4], wb[4];
     int m = cnt;
     for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
     const int b0 = __shfl(b, 0);
     const bool uniform = __all(b == b0);
+    const bool live = i - (threadIdx.x & 63) < (long long)c.B * HW;      // the wave has pixels
     if (uniform) {
-        if ((threadIdx.x & 63) == 0 && i - (threadIdx.x & 63) < (long long)c.B * HW) atomicMax(w.iters_raw + b0, m);
-    } else if (i < (long long)c.B * HW) {
-        atomicMax(w.iters_raw + b, cnt);
+        if ((threadIdx.x & 63) == 0) { wmax[threadIdx.x >> 6] = live ? m : 0; wb[threadIdx.x >> 6] = live ? b0 : -1; }
+    } else {
+        if (i < (long long)c.B * HW) atomicMax(w.iters_raw + (size_t)b * MAXSLOTS + blockIdx.x % MAXSLOTS, cnt);
+        if ((threadIdx.x & 63) == 0) { wmax[threadIdx.x >> 6] = 0; wb[threadIdx.x >> 6] = -1; }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // waves of one batch element combine; a workgroup spans at most two elements
+        for (int k = 0; k < 4; ++k) {
+            if (wb[k] < 0) continue;
+            int mk = wmax[k];
+            for (int l = k + 1; l < 4; ++l)
+                if (wb[l] == wb[k]) { mk = max(mk, wmax[l]); wb[l] = -1; }
+            atomicMax(w.iters_raw + (size_t)wb[k] * MAXSLOTS + blockIdx.x % MAXSLOTS, mk);
+        }
     }
 }
 
@@ -187,7 +205,8 @@ __global__ void v2e_iters_kernel(Call c, Scratch w) {
     if (threadIdx.x != 0) return;
     int mx = 0;
     for (int b = 0; b < c.B; ++b) {
-        const int r = w.iters_raw[b];
+        int r = 0;
+        for (int k = 0; k < MAXSLOTS; ++k) r = max(r, w.iters_raw[(size_t)b * MAXSLOTS + k]);
         mx = max(mx, r);                                       // max_num_iters (:417)
         const int ni = r == 0 ? 1 : r;                         // :426
         w.num_iters[b] = ni;
@@ -306,7 +325,7 @@ WsLayout carve_ws(void *base, int B, int H, int W, int nb) {
     };
     L.sc.counts = static_cast<int *>(take(n * 4));
     L.sc.pol = static_cast<float *>(take(n * 4));
-    L.sc.iters_raw = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * 4));
+    L.sc.iters_raw = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * MAXSLOTS * 4));
     L.sc.num_iters = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * 4));
     L.sc.ts_step = static_cast<float *>(take(CISTA_V2E_MAX_BATCH * 4));
     L.sc.meta = static_cast<int *>(take(16));
@@ -403,7 +422,7 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
     hs->draw += 2 * (unsigned long long)F + 16;
     for (int n = 1; n < F; ++n) {
         const float dt = c.tf[n] - hs->t_previous;                                 // :352
-        if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+        if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * MAXSLOTS * 4, st) != hipSuccess) return CISTA_ERR_HIP;
         hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
         hipLaunchKernelGGL(v2e_iters_kernel, dim3(1), dim3(64), 0, st, c, L.sc);
         hipLaunchKernelGGL(v2e_emit_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, voxels, n, dt);
