@@ -48,7 +48,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
-    p.add_argument("--batch_size", "--batch", dest="batch", type=int, default=64, help="sequences per GPU")
+    # 256 sequences x 15 frames of 180x240 state and voxels are ~4 GB of the 288 GB HBM; the tiles
+    # of the last dispatch round are then a smaller share than at 64 (sweep: 7918 / 8061 / 8143 /
+    # 8147 frames/s at B = 64 / 128 / 256 / 512)
+    p.add_argument("--batch_size", "--batch", dest="batch", type=int, default=256, help="sequences per GPU")
     p.add_argument("-s", "--len_sequence", "--len-seq", dest="len_seq", type=int, default=15)
     p.add_argument("--image_dim", nargs=2, type=int, default=None, metavar=("H", "W"),
                    help="frame height and width (default 180 240; v2e2v mode 720 1280)")
