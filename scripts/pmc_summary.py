@@ -13,7 +13,7 @@ def short(name):
     if m:
         return "conv<" + m.group(1).replace(" ", "") + ">"
     m = re.search(r"cista::(\w+)", name)
-    return m.group(1) if m else name[:40]
+    return "cista::" + m.group(1) if m else name[:40]
 
 
 def main(pattern):

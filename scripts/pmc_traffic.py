@@ -35,7 +35,7 @@ def layer_of(name):
         return "input", name.split("(")[0].replace("void ", "")
     if "s2d_input_kernel" in name:
         return "input+W0:s2d", name.split("(")[0].replace("void ", "")
-    if "input_w0_kernel" in name:
+    if "input_w0_kernel" in name or "input_border_kernel" in name:
         return "input+W0:border", name.split("(")[0].replace("void ", "")
     if "final_q_kernel" in name or "final_stage_kernel" in name:
         return "final", name.split("(")[0]

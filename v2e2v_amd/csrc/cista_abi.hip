@@ -413,6 +413,12 @@ inline bool s2d_input(const cista_config &cfg) { return CISTA_S2D_IN && cfg.num_
 #define CISTA_S2D_DIRECT 1
 #endif
 
+// ... and its border pixels by per-sample strip segments (input_border_kernel; 0: the
+// class-major input_w0_kernel grid)
+#ifndef CISTA_BORDER_STRIPS
+#define CISTA_BORDER_STRIPS 1
+#endif
+
 // the upsample conv's wave holds all C output channels (WN == 1) for C = 32 and 64
 inline bool up_q_path(int C) { return C == 64 || C == 32; }
 // ... and for C = 64 it runs phase-decomposed over the half-res input
@@ -474,6 +480,17 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                     if (const int sc = launch_conv<STAGE_S1, EPI_BIAS, 1>(a, f.st)) return sc;
                     fa.border_only = 1;
                     most = (long)B * (h > w ? h : w);
+                }
+                if (fa.border_only && CISTA_BORDER_STRIPS) {
+                    // per-sample strip segments: a sample's border inputs are fetched once
+                    const dim3 gb((unsigned)border_blocks(B, h, w), (unsigned)((C / 32 + 1) / 2));
+                    switch (f.cfg->num_bins) {
+#define NBCASE(n)                                                                          \
+    case n: hipLaunchKernelGGL(input_border_kernel<n>, gb, dim3(256), 0, f.st, fa); break;
+                        NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7)
+#undef NBCASE
+                    }
+                    return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
                 }
                 const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9,
                               fa.border_only ? C / 32 : 1);
