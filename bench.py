@@ -567,6 +567,12 @@ def main():
             roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
             if tl and tj.get("lib_sha256") == sha:
                 roofline["traffic"] = tl["hbm_bytes_per_launch"]
+                # the same launch against the HBM roof: the ISTA / Dg convs move as many bytes
+                # per FLOP as the two roofs balance, so their time is bounded by the sum of the
+                # two fractions when staging / epilogue and MFMAs do not overlap
+                gbps = tl["hbm_bytes_per_launch"] / (dom["ms"] * 1e-3) / 1e9
+                roofline["hbm_achieved_GBps"] = round(gbps, 1)
+                roofline["hbm_frac"] = round(gbps / (HBM_TBPS * 1e3), 4)
             else:       # measured on another build (or not this kernel): never quote stale bytes
                 roofline["traffic_note"] = ("no PMC traffic of this build's " + dom_name + " kernel in "
                                             + roofline["traffic_source"])

@@ -707,13 +707,25 @@ __global__ __launch_bounds__(256) void upsample2x_kernel(const float *x, float *
     *(float4 *)(up + (size_t)pix * C + 4 * q) = r;
 }
 
-// dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9)
-__global__ __launch_bounds__(256) void reduce_partials_kernel(const float *partial, int nsplit, long n,
-                                                              float *dst, float sign, int accumulate) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+// dW (+)= sign * sum over splits of partial  (n = Cout*Cin*9); threads n .. n + nb - 1 do the
+// bias gradient db from bpartial in the same launch.  The split sum is latency-bound (each
+// thread walks nsplit rows): 16 rows are loaded per round, then added in the order of four
+// interleaved accumulators (row k into s[k % 4]), so the result does not depend on the batching.
+__device__ __forceinline__ float sum_splits(const float *partial, int nsplit, long n, long i) {
     float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
     int k = 0;
+    for (; k + 16 <= nsplit; k += 16) {
+        float v[16];
+#pragma unroll
+        for (int u = 0; u < 16; ++u) v[u] = partial[(size_t)(k + u) * n + i];
+#pragma unroll
+        for (int u = 0; u < 16; u += 4) {
+            s0 += v[u];
+            s1 += v[u + 1];
+            s2 += v[u + 2];
+            s3 += v[u + 3];
+        }
+    }
     for (; k + 4 <= nsplit; k += 4) {
         s0 += partial[(size_t)k * n + i];
         s1 += partial[(size_t)(k + 1) * n + i];
@@ -721,7 +733,22 @@ __global__ __launch_bounds__(256) void reduce_partials_kernel(const float *parti
         s3 += partial[(size_t)(k + 3) * n + i];
     }
     for (; k < nsplit; ++k) s0 += partial[(size_t)k * n + i];
-    dst[i] = (accumulate ? dst[i] : 0.0f) + sign * ((s0 + s1) + (s2 + s3));
+    return (s0 + s1) + (s2 + s3);
+}
+
+__global__ __launch_bounds__(256) void reduce_partials_kernel(const float *partial, int nsplit, long n,
+                                                              float *dst, float sign, int accumulate,
+                                                              const float *bpartial = nullptr, long nb = 0,
+                                                              float *bdst = nullptr) {
+    long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) {
+        i -= n;
+        if (i >= nb) return;
+        partial = bpartial;
+        n = nb;
+        dst = bdst;
+    }
+    dst[i] = (accumulate ? dst[i] : 0.0f) + sign * sum_splits(partial, nsplit, n, i);
 }
 
 // --------------------------------------------------------------------------------------------
