@@ -1021,7 +1021,14 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
         d.mask = sv.u; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = 1; d.Cin = C;
         d.accumulate = 0;
-        CHECK(dgrad_vec(k, d, P.final_w));                                              // g_U (ReLU'd)
+        if (C % 8 == 0) {                                                               // g_U (ReLU'd)
+            hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * 9), dim3(256), 0, st, P.final_w, 1, C, ws.wT);
+            hipLaunchKernelGGL(dgrad_final_kernel, g1d(HW * (C / 8)), dim3(256), 0, st, (const float *)ws.gpre,
+                               (const float *)ws.wT, (const float *)sv.u, ws.gU, B, H, W, C);
+            CHECK(hip_ok());
+        } else {
+            CHECK(dgrad_vec(k, d, P.final_w));
+        }
         // upsample conv wgrad as a stride-1 wgrad over the materialised up(h) (in dxpF, which
         // the dgrad below overwrites); the gradient scale is shared with that dgrad
         const float *gsu = grad_scale(k, ws.gU, HW * C);
@@ -1069,12 +1076,16 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         const float *xk = sv.xs + (size_t)it * hw * C;
         const float *zk = sv.zl;
         if (it > 0) {
-            hipLaunchKernelGGL(softshrink_fwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st,
+            hipLaunchKernelGGL(softshrink_fwd4_kernel, g1d(hw * 2 * C / 4), dim3(256), 0, st,
                                sv.v + (size_t)(it - 1) * hw * 2 * C, lam, ws.zk, hw, 2 * C);
             zk = ws.zk;
         }
-        hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                           lam, ws.gv, ws.dlp, hw, 2 * C);
+        if (1024 % (2 * C) == 0)
+            hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
+                               lam, ws.gv, ws.dlp, hw, 2 * C);
+        else
+            hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
+                               lam, ws.gv, ws.dlp, hw, 2 * C);
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
         gsc = grad_scale(k, ws.gv, hw * 2 * C);

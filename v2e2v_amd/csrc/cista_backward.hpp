@@ -876,6 +876,43 @@ __global__ __launch_bounds__(256) void dgrad_vec_kernel(const DgradSmallArgs a, 
     *dst = s;
 }
 
+// final_conv dgrad (Cout 1, stride 1, reflect padding) with the upsample ReLU mask: dX (B,H,W,C)
+// = [u > 0] * sum over (P, t) with reflect(P + t - 1) == Q of G[P] W[t][c].  Thread = (pixel, 8
+// channels): two float4 weight loads ([9][C] layout, L1-resident) per tap feed 8 FMAs; the
+// general dgrad_vec_kernel spent 4 threads and 64-bit index math per such group (211 us at B=8).
+__global__ __launch_bounds__(256) void dgrad_final_kernel(const float *G, const float *WT, const float *mask,
+                                                          float *dX, int B, int H, int W, int C) {
+    const int c8 = C >> 3;
+    const long total = (long)B * H * W * c8;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx >= total) return;
+    const int c = (int)(idx % c8) * 8;
+    const long pix = idx / c8;
+    const int plane = H * W;
+    const int b = (int)(pix / plane), r = (int)(pix - (long)b * plane);
+    const int y = r / W, x = r - y * W;
+    int Py[6], Ty[6], Px[6], Tx[6];
+    const int ny = refl_taps(y, H, H, 1, Py, Ty), nx = refl_taps(x, W, W, 1, Px, Tx);
+    const float *g = G + (size_t)b * plane;
+    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+    for (int i = 0; i < ny; ++i)
+        for (int j = 0; j < nx; ++j) {
+            const float gv = g[Py[i] * W + Px[j]];
+            const float *w = WT + (Ty[i] * 3 + Tx[j]) * C + c;
+            const float4 w0 = *reinterpret_cast<const float4 *>(w), w1 = *reinterpret_cast<const float4 *>(w + 4);
+            s0.x = fmaf(gv, w0.x, s0.x); s0.y = fmaf(gv, w0.y, s0.y); s0.z = fmaf(gv, w0.z, s0.z); s0.w = fmaf(gv, w0.w, s0.w);
+            s1.x = fmaf(gv, w1.x, s1.x); s1.y = fmaf(gv, w1.y, s1.y); s1.z = fmaf(gv, w1.z, s1.z); s1.w = fmaf(gv, w1.w, s1.w);
+        }
+    const size_t o = (size_t)pix * C + c;
+    const float4 m0 = *reinterpret_cast<const float4 *>(mask + o), m1 = *reinterpret_cast<const float4 *>(mask + o + 4);
+    s0.x = m0.x > 0.0f ? s0.x : 0.0f; s0.y = m0.y > 0.0f ? s0.y : 0.0f;
+    s0.z = m0.z > 0.0f ? s0.z : 0.0f; s0.w = m0.w > 0.0f ? s0.w : 0.0f;
+    s1.x = m1.x > 0.0f ? s1.x : 0.0f; s1.y = m1.y > 0.0f ? s1.y : 0.0f;
+    s1.z = m1.z > 0.0f ? s1.z : 0.0f; s1.w = m1.w > 0.0f ? s1.w : 0.0f;
+    *reinterpret_cast<float4 *>(dX + o) = s0;
+    *reinterpret_cast<float4 *>(dX + o + 4) = s1;
+}
+
 // W0 (stride 2) dgrad on the zero-padded input domain: dxp (B, H+2, W+2, Cin) gets
 //   dxp[qy][qx] = sum over taps (ty, tx) with qy = 2 Py + ty, qx = 2 Px + tx of G[Py][Px] . W[t]
 // (reflect folding follows in fold_reflect_kernel).  A thread owns 4 input channels of 4
@@ -1000,6 +1037,54 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
         for (int k = threadIdx.x; k < 256; k += C) s += red[k];
         dl_partial[(size_t)blockIdx.x * C + threadIdx.x] = s;
     }
+}
+
+// softshrink_bwd_kernel over float4 channel groups (1024 % C == 0): the same gv and, per
+// workgroup, the same dlambda partials up to the order of the per-channel sums
+__global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, const float *v,
+                                                              const float *lam, float *gv,
+                                                              float *dl_partial, long npix, int C) {
+    __shared__ float4 red[256];
+    const int cq = C >> 2, c = (threadIdx.x % cq) * 4;
+    const float4 l = *reinterpret_cast<const float4 *>(lam + c);
+    const long total = npix * cq;
+    const float4 *v4 = reinterpret_cast<const float4 *>(v), *g4 = reinterpret_cast<const float4 *>(gz);
+    float4 *o4 = reinterpret_cast<float4 *>(gv);
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto one = [](float vv, float g, float lv, float &a) {
+        const bool up = vv > lv, dn = vv < -lv;
+        a += g * ((dn ? 1.0f : 0.0f) - (up ? 1.0f : 0.0f));
+        return g * ((up ? 1.0f : 0.0f) + (dn ? 1.0f : 0.0f));
+    };
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+        const float4 vv = v4[i], g = g4[i];
+        float4 r;
+        r.x = one(vv.x, g.x, l.x, acc.x);
+        r.y = one(vv.y, g.y, l.y, acc.y);
+        r.z = one(vv.z, g.z, l.z, acc.z);
+        r.w = one(vv.w, g.w, l.w, acc.w);
+        o4[i] = r;
+    }
+    red[threadIdx.x] = acc;
+    __syncthreads();
+    if ((int)threadIdx.x < cq) {
+        float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int k = threadIdx.x; k < 256; k += cq) {
+            s.x += red[k].x; s.y += red[k].y; s.z += red[k].z; s.w += red[k].w;
+        }
+        *reinterpret_cast<float4 *>(dl_partial + (size_t)blockIdx.x * C + 4 * threadIdx.x) = s;
+    }
+}
+
+// z = softshrink(v, lambda) over float4 channel groups (C % 4 == 0)
+__global__ void softshrink_fwd4_kernel(const float *v, const float *lam, float *z, long npix, int C) {
+    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int cq = C >> 2;
+    if (i >= npix * cq) return;
+    const int c = (int)(i % cq) * 4;
+    const float4 x = reinterpret_cast<const float4 *>(v)[i];
+    reinterpret_cast<float4 *>(z)[i] = make_float4(softshrink_(x.x, lam[c]), softshrink_(x.y, lam[c + 1]),
+                                                   softshrink_(x.z, lam[c + 2]), softshrink_(x.w, lam[c + 3]));
 }
 
 // dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel;
