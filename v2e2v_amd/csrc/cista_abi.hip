@@ -991,11 +991,14 @@ int dgrad_conv(Bwd &k, int id, const float *G, float *dxp, const float *sc = nul
     return launch_conv<STAGE_ZP2, EPI_BIAS, 1>(a, k.st);
 }
 
+// add: dst = add + fold (copy-free identity path; NULL add with accumulate 0 is plain dst = fold);
+// dst2: a second destination receiving dst2 += fold from the same pass over src
 int fold(Bwd &k, const float *src, int Cs, int sc0, float *dst, int Cd, int dc0, int n, int H, int W,
-         float scale, int accumulate, const float *mask) {
+         float scale, int accumulate, const float *mask, const float *add = nullptr, float *dst2 = nullptr) {
     FoldArgs f;
     f.src = src; f.Cs = Cs; f.sc0 = sc0; f.dst = dst; f.Cd = Cd; f.dc0 = dc0; f.n = n;
     f.B = k.B; f.H = H; f.W = W; f.scale = scale; f.accumulate = accumulate; f.mask = mask;
+    f.add = add; f.dst2 = dst2;
     hipLaunchKernelGGL(fold_reflect_kernel, g1d((long)k.B * H * W * (n / 4)), dim3(256), 0, k.st, f);
     return hip_ok();
 }
@@ -1057,8 +1060,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     gsc = grad_scale(k, ws.gy, hw * C);
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
     CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
-    CHECK(copy_or_zero(ws.gz, g.g_z, (size_t)hw * 2 * C, st));
-    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr, g.g_z));   // g_z + fold
     // ---- 5. ISTA, reversed (tied D, P, lambda accumulate over iterations) -------------------
     const float *lam = blob<float>(k.packed, k.L.lambda);
     if (D == 0) {
@@ -1091,14 +1093,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         gsc = grad_scale(k, ws.gv, hw * 2 * C);
         CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b, gsc));
         CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr));
-        CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1));   // gx1 += too
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
         gsc = grad_scale(k, ws.gxk, hw * C);
         CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b, gsc));
         CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp, gsc));
-        CHECK(copy_or_zero(ws.gz, ws.gv, (size_t)hw * 2 * C, st));          // identity path
-        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 1, nullptr));
+        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, ws.gv));   // identity path + fold
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
         hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
                            pg.lambda, it != D - 1);

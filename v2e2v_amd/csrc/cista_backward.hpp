@@ -30,6 +30,8 @@ struct FoldArgs {
     float scale;
     int accumulate;        // 0: dst = fold, 1: dst += fold
     const float *mask;     // optional, applied to the result (NHWC, Cd channels)
+    const float *add;      // optional (accumulate == 0): dst = add + fold (add laid out as dst)
+    float *dst2;           // optional second destination (laid out as dst): dst2 += fold
 };
 
 __device__ __forceinline__ int refl_sources(int i, int n, int (&out)[3]) {
@@ -60,11 +62,18 @@ __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
             const float4 v = *(const float4 *)(a.src + (((size_t)b * (a.H + 2) + ys[i]) * (a.W + 2) + xs[j]) * a.Cs + a.sc0 + c);
             s.x += v.x; s.y += v.y; s.z += v.z; s.w += v.w;
         }
-    float4 *d = (float4 *)(a.dst + (size_t)pix * a.Cd + a.dc0 + c);
-    float4 r = make_float4(s.x * a.scale, s.y * a.scale, s.z * a.scale, s.w * a.scale);
-    if (a.accumulate) {
-        const float4 o = *d;
-        r.x += o.x; r.y += o.y; r.z += o.z; r.w += o.w;
+    const size_t od = (size_t)pix * a.Cd + a.dc0 + c;
+    float4 *d = (float4 *)(a.dst + od);
+    const float4 f = make_float4(s.x * a.scale, s.y * a.scale, s.z * a.scale, s.w * a.scale);
+    float4 r = f;
+    if (a.accumulate || a.add) {
+        const float4 o = a.accumulate ? *d : *(const float4 *)(a.add + od);
+        r.x = o.x + f.x; r.y = o.y + f.y; r.z = o.z + f.z; r.w = o.w + f.w;
+    }
+    if (a.dst2) {
+        float4 *d2 = (float4 *)(a.dst2 + od);
+        const float4 o = *d2;
+        *d2 = make_float4(o.x + f.x, o.y + f.y, o.z + f.z, o.w + f.w);
     }
     if (a.mask) {
         const float4 m = *(const float4 *)(a.mask + (size_t)pix * a.Cd + a.dc0 + c);
