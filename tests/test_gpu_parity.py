@@ -291,3 +291,26 @@ def test_determinism_and_batch_independence():
         ra, sa = m(vox[2:3], prev[2:3], None)
     assert torch.equal(r1, r2) and torch.equal(s1[1], s2[1])
     assert torch.equal(r1[2:3], ra) and torch.equal(s1[2][1][2:3], sa[2][1])
+
+
+@pytest.mark.parametrize("H,W", [(20, 300), (300, 20)])
+def test_border_segments_and_corner_blocks(H, W):
+    """The input stage's border pass (input_border_kernel): strips longer than one 128-pixel
+    segment (w or h = 150) and corner workgroups covering 64 samples each (B = 130: blocks of 64,
+    64, 2).  Every sample of the batched frame equals its own B=1 run bit for bit, and one sample
+    matches the oracle."""
+    params = fx.stress_params(32, 1, 5, seed=77)
+    m = make_model(C=32, depth=1, params=params)
+    B = 130
+    rng = np.random.default_rng(H)
+    vox = rng.standard_normal((B, 5, H, W)).astype(np.float32)
+    prev = rng.random((B, 1, H, W)).astype(np.float32)
+    with torch.no_grad():
+        r, s = m(gpu(vox), gpu(prev), None)
+        for i in (0, 63, 64, 129):
+            ri, si = m(gpu(vox[i:i + 1]), gpu(prev[i:i + 1]), None)
+            assert torch.equal(r[i:i + 1], ri), i
+            assert torch.equal(s[1][i:i + 1], si[1]), i
+    o_rec, o_st = CistaLSTCOracle(params, 1).forward(vox[129:130], prev[129:130], None)
+    assert rel_err(r[129:130].cpu().numpy(), o_rec) < TOL
+    assert rel_err(s[1][129:130].cpu().numpy(), o_st[1]) < TOL
