@@ -1139,9 +1139,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
     {
         // padded-domain stride-2 dgrad into dxpF, then reflect-fold into gxfull
-        const int Hp = H + 2, Wp = W + 2, ngx = (((Wp + 1) / 2) + 3) / 4;
+        const int Hp = H + 2, Wp = W + 2, ngx = (((Wp + 1) / 2) + S2_NJ - 1) / S2_NJ;
         hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * C * 9), dim3(256), 0, st, P.W0_w, C, C, ws.wT);
-        hipLaunchKernelGGL(dgrad_s2_kernel, g1d((long)B * Hp * 2 * ngx * (C / 4)), dim3(256), 0, st,
+        hipLaunchKernelGGL(dgrad_s2_kernel, g1d((long)B * Hp * 2 * ngx * (C / 8)), dim3(256), 0, st,
                            (const float *)ws.gx1, C, 0, (const float *)ws.wT, C, C, B, h, w, ws.dxpF, Hp, Wp);
         CHECK(fold(k, ws.dxpF, C, 0, gxfull, C, 0, C, H, W, 1.0f, 0, nullptr));
     }

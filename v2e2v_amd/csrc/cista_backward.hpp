@@ -924,17 +924,20 @@ __global__ __launch_bounds__(256) void dgrad_final_kernel(const float *G, const 
 
 // W0 (stride 2) dgrad on the zero-padded input domain: dxp (B, H+2, W+2, Cin) gets
 //   dxp[qy][qx] = sum over taps (ty, tx) with qy = 2 Py + ty, qx = 2 Px + tx of G[Py][Px] . W[t]
-// (reflect folding follows in fold_reflect_kernel).  A thread owns 4 input channels of 4
-// same-parity columns qx = px + 2 (4 xg + j), which share the tap set, so one float4 weight
-// load feeds 16 FMAs.  G (B, h, w, Gc) NHWC, WT [9][Cout][Cin]; Cin, Cout, Gc, Goff % 4 == 0.
+// (reflect folding follows in fold_reflect_kernel).  A thread owns 8 input channels of NJ = 8
+// same-parity columns qx = px + 2 (NJ xg + j), which share the tap set: per 4 output channels a
+// tap costs 8 weight float4 + NJ gradient float4 loads for 256 FMAs (the 4 x 4 version was bound
+// by the CU's vector-memory address rate: 8 loads per 64 FMAs, 250 us at B = 8).
+// G (B, h, w, Gc) NHWC, WT [9][Cout][Cin]; Cin % 8, Cout, Gc, Goff % 4 == 0.
+constexpr int S2_NJ = 8;
 __global__ __launch_bounds__(256) void dgrad_s2_kernel(const float *G, int Gc, int Goff, const float *WT, int Cout,
                                                        int Cin, int B, int h, int w, float *dxp, int Hp, int Wp) {
-    const int cq = Cin >> 2;
-    const int ngx = (((Wp + 1) >> 1) + 3) >> 2;
+    const int cq = Cin >> 3;
+    const int ngx = (((Wp + 1) >> 1) + S2_NJ - 1) / S2_NJ;
     const long total = (long)B * Hp * 2 * ngx * cq;
     long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const int ci = (int)(idx % cq) * 4;
+    const int ci = (int)(idx % cq) * 8;
     idx /= cq;
     const int xg = (int)(idx % ngx);
     idx /= ngx;
@@ -943,46 +946,57 @@ __global__ __launch_bounds__(256) void dgrad_s2_kernel(const float *G, int Gc, i
     const int qy = (int)(idx % Hp);
     const int b = (int)(idx / Hp);
     const int cnt = (Wp - px + 1) >> 1;
-    if (4 * xg >= cnt) return;
-    float4 acc[4];
+    if (S2_NJ * xg >= cnt) return;
+    float4 acc[S2_NJ][2];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int j = 0; j < S2_NJ; ++j) acc[j][0] = acc[j][1] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int ty = 0; ty < 3; ++ty) {
         if ((qy - ty) & 1) continue;
         const int Py = (qy - ty) >> 1;
         if (Py < 0 || Py >= h) continue;
         const float *grow = G + ((size_t)b * h + Py) * w * Gc + Goff;
         for (int tx = px; tx < 3; tx += 2) {
-            const int pofs = 4 * xg + ((px - tx) >> 1);     // Px of column j = pofs + j
-            bool ok[4];
-            const float *gp[4];
+            const int pofs = S2_NJ * xg + ((px - tx) >> 1);     // Px of column j = pofs + j
+            bool ok[S2_NJ];
+            const float *gp[S2_NJ];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) {
+            for (int j = 0; j < S2_NJ; ++j) {
                 const int Px = pofs + j;
-                ok[j] = Px >= 0 && Px < w && 4 * xg + j < cnt;
+                ok[j] = Px >= 0 && Px < w && S2_NJ * xg + j < cnt;
                 gp[j] = grow + (size_t)(ok[j] ? Px : 0) * Gc;
             }
             const float *wt = WT + (size_t)(ty * 3 + tx) * Cout * Cin + ci;
             for (int co = 0; co < Cout; co += 4) {
-                float4 wv[4];
+                float4 wv[4][2];
 #pragma unroll
-                for (int k = 0; k < 4; ++k) wv[k] = *reinterpret_cast<const float4 *>(wt + (size_t)(co + k) * Cin);
+                for (int k = 0; k < 4; ++k) {
+                    wv[k][0] = *reinterpret_cast<const float4 *>(wt + (size_t)(co + k) * Cin);
+                    wv[k][1] = *reinterpret_cast<const float4 *>(wt + (size_t)(co + k) * Cin + 4);
+                }
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
+                for (int j = 0; j < S2_NJ; ++j) {
                     float4 g = *reinterpret_cast<const float4 *>(gp[j] + co);
                     if (!ok[j]) g = make_float4(0.f, 0.f, 0.f, 0.f);
-                    acc[j].x = fmaf(g.x, wv[0].x, fmaf(g.y, wv[1].x, fmaf(g.z, wv[2].x, fmaf(g.w, wv[3].x, acc[j].x))));
-                    acc[j].y = fmaf(g.x, wv[0].y, fmaf(g.y, wv[1].y, fmaf(g.z, wv[2].y, fmaf(g.w, wv[3].y, acc[j].y))));
-                    acc[j].z = fmaf(g.x, wv[0].z, fmaf(g.y, wv[1].z, fmaf(g.z, wv[2].z, fmaf(g.w, wv[3].z, acc[j].z))));
-                    acc[j].w = fmaf(g.x, wv[0].w, fmaf(g.y, wv[1].w, fmaf(g.z, wv[2].w, fmaf(g.w, wv[3].w, acc[j].w))));
+#pragma unroll
+                    for (int hh = 0; hh < 2; ++hh) {
+                        float4 &A = acc[j][hh];
+                        A.x = fmaf(g.x, wv[0][hh].x, fmaf(g.y, wv[1][hh].x, fmaf(g.z, wv[2][hh].x, fmaf(g.w, wv[3][hh].x, A.x))));
+                        A.y = fmaf(g.x, wv[0][hh].y, fmaf(g.y, wv[1][hh].y, fmaf(g.z, wv[2][hh].y, fmaf(g.w, wv[3][hh].y, A.y))));
+                        A.z = fmaf(g.x, wv[0][hh].z, fmaf(g.y, wv[1][hh].z, fmaf(g.z, wv[2][hh].z, fmaf(g.w, wv[3][hh].z, A.z))));
+                        A.w = fmaf(g.x, wv[0][hh].w, fmaf(g.y, wv[1][hh].w, fmaf(g.z, wv[2][hh].w, fmaf(g.w, wv[3][hh].w, A.w))));
+                    }
                 }
             }
         }
     }
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-        const int qx = px + 2 * (4 * xg + j);
-        if (qx < Wp) *reinterpret_cast<float4 *>(dxp + (((size_t)b * Hp + qy) * Wp + qx) * Cin + ci) = acc[j];
+    for (int j = 0; j < S2_NJ; ++j) {
+        const int qx = px + 2 * (S2_NJ * xg + j);
+        if (qx < Wp) {
+            float *o = dxp + (((size_t)b * Hp + qy) * Wp + qx) * Cin + ci;
+            *reinterpret_cast<float4 *>(o) = acc[j][0];
+            *reinterpret_cast<float4 *>(o + 4) = acc[j][1];
+        }
     }
 }
 
