@@ -482,11 +482,17 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                     most = (long)B * (h > w ? h : w);
                 }
                 if (fa.border_only && CISTA_BORDER_STRIPS) {
-                    // per-sample strip segments: a sample's border inputs are fetched once
-                    const dim3 gb((unsigned)border_blocks(B, h, w), (unsigned)((C / 32 + 1) / 2));
+                    // per-sample strip segments: a sample's border inputs are fetched once; 8
+                    // channels per wave at small batch (latency), 32 otherwise
+                    const bool small = B < 32;
+                    const int ct = small ? 8 : 32;
+                    const dim3 gb((unsigned)((long)B * border_segments(h, w)), (unsigned)((C / ct + 1) / 2));
                     switch (f.cfg->num_bins) {
 #define NBCASE(n)                                                                          \
-    case n: hipLaunchKernelGGL(input_border_kernel<n>, gb, dim3(256), 0, f.st, fa); break;
+    case n:                                                                                \
+        if (small) hipLaunchKernelGGL((input_border_kernel<n, 8>), gb, dim3(256), 0, f.st, fa);  \
+        else hipLaunchKernelGGL((input_border_kernel<n, 32>), gb, dim3(256), 0, f.st, fa);       \
+        break;
                         NBCASE(1) NBCASE(2) NBCASE(3) NBCASE(4) NBCASE(5) NBCASE(6) NBCASE(7)
 #undef NBCASE
                     }

@@ -1268,83 +1268,46 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
 }
 
 // Border pixels of the composed input stage after the MFMA interior: one
-// workgroup per (sample, strip segment), so that a sample's border inputs are fetched once
-// and not once per class and channel half (at B = 256 the class-major grid above re-fetched
-// them from HBM: 805 MB per launch).  Strips per sample: the top and bottom output rows and the
-// left and right output columns without their corners, each cut into segments of BORDER_SEG
-// pixels, so every segment is one reflect class.  The segment's input window (<= 5 rows or
-// columns of every plane) is staged in LDS with coalesced loads; a wave then computes 64
-// pixels x 32 output channels with the class's composed weights as wave-uniform scalar loads
-// (wave = (pixel chunk, channel quarter); gridDim.y covers C / 64 quarter pairs).  The four
-// corner classes are extra workgroups after the segments (2 corners x 2 quarters per workgroup,
-// lane = sample of a 64-sample block), inputs read straight from the planes.
+// workgroup per (sample, strip segment, channel range), so that a sample's border inputs are
+// fetched once and not once per class and channel half (at B = 256 the class-major grid above
+// re-fetched them from HBM: 805 MB per launch).  Strips per sample: the top and bottom output
+// rows and the left and right output columns without their corners, each cut into segments of
+// BORDER_SEG pixels, so every segment is one reflect class.  The segment's input window (<= 5
+// rows or columns of every plane) is staged in LDS with coalesced loads; wave = (64 pixels, CT
+// output channels) with the class's composed weights as wave-uniform scalar loads.  CT = 32 for
+// throughput, 8 at small batch (4x the waves, a quarter of each wave's serial FMA chain: the
+// B = 1 frame is latency-bound).  The four corner pixels ride on the first / last segment of
+// their row strip (the strip is widened to their windows): one wave per corner, lane = output
+// channel, inputs as LDS broadcasts and per-lane coalesced weight loads (150 FMAs per wave).
 constexpr int BORDER_SEG = 128;
+__host__ __device__ inline int border_row_segments(int w) {
+    const int n = (w - 2 + BORDER_SEG - 1) / BORDER_SEG;
+    return n < 1 ? 1 : n;                           // >= 1: the corners ride on it
+}
 __host__ __device__ inline int border_segments(int h, int w) {
-    return 2 * ((w - 2 + BORDER_SEG - 1) / BORDER_SEG) + 2 * ((h - 2 + BORDER_SEG - 1) / BORDER_SEG);
-}
-// grid: x = B * segments + 2 corner workgroups per 64 samples, y = pairs of 32-channel quarters
-__host__ __device__ inline long border_blocks(int B, int h, int w) {
-    return (long)B * border_segments(h, w) + 2L * ((B + 63) / 64);
+    return 2 * border_row_segments(w) + 2 * ((h - 2 + BORDER_SEG - 1) / BORDER_SEG);
 }
 
-// one 32-channel pass of the composed 5x5 map for the lane's pixel; every load precedes every
-// store of the kernel, so the wave-uniform weight loads stay scalar (s_load)
-template <int K, typename In>
-__device__ __forceinline__ void border_pass(float (&acc)[32], const float *E, const float *bias, int C, In in) {
-#pragma unroll
-    for (int i = 0; i < 32; ++i) acc[i] = bias[i];
-    for (int t = 0; t < 25; ++t) {
-        const float *wt = E + (size_t)t * K * C;
-#pragma unroll
-        for (int ci = 0; ci < K; ++ci) {
-            const float vv = in(t, ci);
-#pragma unroll
-            for (int i = 0; i < 32; ++i) acc[i] = fmaf(vv, wt[(size_t)ci * C + i], acc[i]);
-        }
-    }
-}
-
-template <int NB>
+template <int NB, int CT>
 __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) {
-    constexpr int K = NB + 1, PITCH_MAX = 2 * BORDER_SEG + 5;       // odd pitch: 2-way at most
+    constexpr int K = NB + 1, PITCH_MAX = 2 * BORDER_SEG + 7;       // odd pitch: 2-way at most
     __shared__ float strip[K * 5 * PITCH_MAX];
     const int h = a.h, w = a.w, H = a.H, W = a.W, C = a.C;
     // wave index through readfirstlane: the weight addresses derive from it and must be known
     // wave-uniform (scalar loads), else the compiler emits a vector load per weight
     const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int q = blockIdx.y * 2 + (wave & 1), q0 = q * 32;         // this wave's channel quarter
+    const int q0 = (blockIdx.y * 2 + (wave & 1)) * CT;              // this wave's output channels
     const size_t plane = (size_t)H * W;
-    const long nsegs = (long)a.B * border_segments(h, w);
-    float acc[32];
-    if (blockIdx.x >= nsegs) {                                      // corners: lane = sample
-        const int cb = (int)(blockIdx.x - nsegs), corner = (cb & 1) * 2 + (wave >> 1);
-        const int b = (cb >> 1) * 64 + lane;
-        const int oy = corner < 2 ? 0 : h - 1, ox = corner & 1 ? w - 1 : 0;
-        const int cls = (oy == 0 ? 0 : 2) * 3 + (ox == 0 ? 0 : 2);
-        if (q0 >= C) return;
-        const int bb = b < a.B ? b : a.B - 1;
-        const float *ev = a.events + (size_t)bb * NB * plane, *im = a.prev + (size_t)bb * plane;
-        border_pass<K>(acc, a.E + (size_t)cls * 25 * K * C + q0, a.bias + q0, C, [&](int t, int ci) {
-            const int y = min(max(2 * oy + t / 5 - 2, 0), H - 1), x = min(max(2 * ox + t % 5 - 2, 0), W - 1);
-            const size_t o = (size_t)y * W + x;
-            return ci < NB ? ev[(size_t)ci * plane + o] : im[o];
-        });
-        if (b < a.B) {
-            float4 *o = (float4 *)(a.out + (((size_t)b * h + oy) * w + ox) * C + q0);
-#pragma unroll
-            for (int i = 0; i < 8; ++i) o[i] = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
-        }
-        return;
-    }
-    const int nrs = (w - 2 + BORDER_SEG - 1) / BORDER_SEG, nseg = border_segments(h, w);
+    const int nrs = border_row_segments(w), nseg = border_segments(h, w);
     const int b = blockIdx.x / nseg;
     int s = blockIdx.x - b * nseg;
     // segment -> (row strip?, fixed coordinate, first pixel, pixel count); pixels 1 .. len - 2
-    bool rowseg;
+    bool rowseg, first = false, last = false;
     int fixed, p0, n;
     if (s < 2 * nrs) {
         rowseg = true;  fixed = s < nrs ? 0 : h - 1;  s = s < nrs ? s : s - nrs;
-        p0 = 1 + s * BORDER_SEG;  n = min(BORDER_SEG, w - 1 - p0);
+        first = s == 0;  last = s == nrs - 1;
+        p0 = 1 + s * BORDER_SEG;  n = max(min(BORDER_SEG, w - 1 - p0), 0);
     } else {
         s -= 2 * nrs;
         const int ncs = (h - 2 + BORDER_SEG - 1) / BORDER_SEG;
@@ -1352,9 +1315,10 @@ __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) 
         p0 = 1 + s * BORDER_SEG;  n = min(BORDER_SEG, h - 1 - p0);
     }
     const int cls = rowseg ? (fixed == 0 ? 1 : 7) : (fixed == 0 ? 3 : 5);
-    // input window: along the strip 2 p0 - 2 .. 2 (p0 + n - 1) + 2, across it 2 fixed - 2 .. + 2
+    // input window: along the strip 2 p0 - 2 .. 2 (p0 + n - 1) + 2 (+ 2 for the last corner),
+    // across it 2 fixed - 2 .. + 2
     const int dim_along = rowseg ? W : H, dim_across = rowseg ? H : W;
-    const int a0 = max(2 * p0 - 2, 0), a1 = min(2 * (p0 + n - 1) + 2, dim_along - 1);
+    const int a0 = max(2 * p0 - 2, 0), a1 = min(2 * (p0 + n - 1) + (last ? 4 : 2), dim_along - 1);
     const int c0 = max(2 * fixed - 2, 0), c1 = min(2 * fixed + 2, dim_across - 1);
     const int ry0 = rowseg ? c0 : a0, nry = rowseg ? c1 - c0 + 1 : a1 - a0 + 1;
     const int cx0 = rowseg ? a0 : c0, ncx = rowseg ? a1 - a0 + 1 : c1 - c0 + 1;
@@ -1366,20 +1330,49 @@ __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) 
         strip[(ci * nry + r) * pitch + x] = src[(size_t)(ry0 + r) * W + cx0 + x];
     }
     __syncthreads();
-    const int chunk = wave >> 1;                                    // 64 pixels of the segment
-    if (chunk * 64 >= n || q0 >= C) return;
-    const int pl = min(chunk * 64 + lane, n - 1);                   // idle lanes repeat the last pixel
-    const int oy = rowseg ? fixed : p0 + pl, ox = rowseg ? p0 + pl : fixed;
-    border_pass<K>(acc, a.E + (size_t)cls * 25 * K * C + q0, a.bias + q0, C, [&](int t, int ci) {
-        // out-of-image window positions carry zero weight; the clamp keeps reads in the strip
+    // strip-relative window position of tap t for output pixel (oy, ox); out-of-image window
+    // positions carry zero weight, the clamp keeps the read inside the strip
+    auto at = [&](int oy, int ox, int t, int ci) {
         const int y = min(max(2 * oy + t / 5 - 2, 0), H - 1) - ry0;
         const int x = min(max(2 * ox + t % 5 - 2, 0), W - 1) - cx0;
         return strip[(ci * nry + y) * pitch + x];
-    });
-    if (chunk * 64 + lane < n) {
-        float4 *o = (float4 *)(a.out + (((size_t)b * h + oy) * w + ox) * C + q0);
+    };
+    const int chunk = wave >> 1;                                    // 64 pixels of the segment
+    if (chunk * 64 < n && q0 < C) {
+        const int pl = min(chunk * 64 + lane, n - 1);               // idle lanes repeat the last pixel
+        const int oy = rowseg ? fixed : p0 + pl, ox = rowseg ? p0 + pl : fixed;
+        const float *E = a.E + (size_t)cls * 25 * K * C + q0;
+        float acc[CT];
 #pragma unroll
-        for (int i = 0; i < 8; ++i) o[i] = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        for (int i = 0; i < CT; ++i) acc[i] = a.bias[q0 + i];
+        for (int t = 0; t < 25; ++t) {
+            const float *wt = E + (size_t)t * K * C;
+#pragma unroll
+            for (int ci = 0; ci < K; ++ci) {
+                const float vv = at(oy, ox, t, ci);
+#pragma unroll
+                for (int i = 0; i < CT; ++i) acc[i] = fmaf(vv, wt[(size_t)ci * C + i], acc[i]);
+            }
+        }
+        if (chunk * 64 + lane < n) {
+            float4 *o = (float4 *)(a.out + (((size_t)b * h + oy) * w + ox) * C + q0);
+#pragma unroll
+            for (int i = 0; i < CT / 4; ++i) o[i] = make_float4(acc[4 * i], acc[4 * i + 1], acc[4 * i + 2], acc[4 * i + 3]);
+        }
+    }
+    // corners (after every scalar weight load above): wave 0 the strip's first corner, wave 1 its
+    // last, lane = output channel
+    if (rowseg && blockIdx.y == 0 && wave < 2 && (wave == 0 ? first : last)) {
+        const int oy = fixed, ox = wave == 0 ? 0 : w - 1;
+        const int ccls = (fixed == 0 ? 0 : 6) + (wave == 0 ? 0 : 2);
+        const float *E = a.E + (size_t)ccls * 25 * K * C;
+        for (int co = lane; co < C; co += 64) {
+            float acc = a.bias[co];
+            for (int t = 0; t < 25; ++t)
+#pragma unroll
+                for (int ci = 0; ci < K; ++ci) acc = fmaf(at(oy, ox, t, ci), E[((size_t)t * K + ci) * C + co], acc);
+            a.out[(((size_t)b * h + oy) * w + ox) * C + co] = acc;
+        }
     }
 }
 
