@@ -1049,7 +1049,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
         CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
         CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
-        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
+        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C / 4), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
                            B, h, w, C, 1);
     } else {
         if (hipMemsetAsync(pg.final_b, 0, 4, st) != hipSuccess ||

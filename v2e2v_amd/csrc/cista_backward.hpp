@@ -1181,27 +1181,38 @@ __device__ __forceinline__ int up_weights(int y, int n, float (&w)[6], int (&Y)[
     return k;
 }
 
+// thread = (half-res pixel, 4 channels): the tap weights once per 4 channels, float4 loads; the
+// per-channel sums keep the scalar kernel's order (rows i, then columns j)
 __global__ void upsample_bwd_kernel(const float *gup, float *gh, int B, int h, int w, int C,
                                     int accumulate) {
-    const long total = (long)B * h * w * C;
+    const int cq = C >> 2;
+    const long total = (long)B * h * w * cq;
     const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
-    const int c = (int)(idx % C);
-    const long pix = idx / C;
-    const int x = (int)(pix % w);
-    const int y = (int)((pix / w) % h);
-    const int b = (int)(pix / ((long)w * h));
+    const int c = (int)(idx % cq) * 4;
+    const long pix = idx / cq;
+    const int plane = h * w;
+    const int b = (int)(pix / plane), r = (int)(pix - (long)b * plane);
+    const int y = r / w, x = r - y * w;
     float wy[6], wx[6];
     int Ys[6], Xs[6];
     const int ny = up_weights(y, h, wy, Ys), nx = up_weights(x, w, wx, Xs);
-    float s = 0.0f;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int i = 0; i < ny; ++i) {
         const float *row = gup + (((size_t)b * 2 * h + Ys[i]) * 2 * w) * C + c;
-        float sr = 0.0f;
-        for (int j = 0; j < nx; ++j) sr += row[(size_t)Xs[j] * C] * wx[j];
-        s += sr * wy[i];
+        float4 sr = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int j = 0; j < nx; ++j) {
+            const float4 v = *reinterpret_cast<const float4 *>(row + (size_t)Xs[j] * C);
+            sr.x += v.x * wx[j]; sr.y += v.y * wx[j]; sr.z += v.z * wx[j]; sr.w += v.w * wx[j];
+        }
+        s.x += sr.x * wy[i]; s.y += sr.y * wy[i]; s.z += sr.z * wy[i]; s.w += sr.w * wy[i];
     }
-    gh[idx] = (accumulate ? gh[idx] : 0.0f) + s;
+    float4 *o = reinterpret_cast<float4 *>(gh + (size_t)pix * C + c);
+    if (accumulate) {
+        const float4 d = *o;
+        s.x = d.x + s.x; s.y = d.y + s.y; s.z = d.z + s.z; s.w = d.w + s.w;
+    }
+    *o = s;
 }
 
 // a = a * (b > 0)   (ReLU mask, elementwise, n floats)
