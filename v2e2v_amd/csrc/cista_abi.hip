@@ -1165,7 +1165,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.G = gxfull; d.Gc = C; d.Goff = half; d.W = P.Wi_w; d.dX = g.g_prev_image; d.Xc = 0; d.Xoff = 0;
         d.mask = nullptr; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = half;
         d.Cin = 1; d.accumulate = 0;
-        hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW), dim3(256), 0, st, d);
+        if (half % 4 == 0 && half <= DC1_MAXC && C % 4 == 0)
+            hipLaunchKernelGGL(dgrad_c1_kernel, dim3((unsigned)((long)B * ((H + 15) / 16) * ((W + 15) / 16))),
+                               dim3(256), 0, st, (const float *)gxfull, C, half, (const float *)P.Wi_w, half,
+                               g.g_prev_image, B, H, W);
+        else
+            hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW), dim3(256), 0, st, d);
     }
     if (g.g_events) {                            // We dgrad: the events' own gradient
         DgradSmallArgs d;

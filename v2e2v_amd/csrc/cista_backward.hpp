@@ -830,6 +830,46 @@ __global__ __launch_bounds__(256) void dgrad_small_kernel(const DgradSmallArgs a
     a.dX[o] = s;
 }
 
+// dgrad_small_kernel for one input channel (Wi: the previous image's gradient), stride 1, with
+// the output gradient staged in LDS: workgroup = 16 x 16 pixel tile, thread = pixel.  The G
+// channels [Goff, Goff + Cout) of the tile's 18 x 18 neighbourhood (every (P, t) of a pixel lies
+// in it, the reflected P = 0 / n - 1 included) are loaded once, coalesced (the per-lane 9-tap
+// gathers of the generic kernel re-fetched G ~15x from HBM: 675 MB per launch at B = 8); pixel
+// stride Cout + 4 floats makes the 16-lane ds_read_b128 groups conflict-free.  Same arithmetic
+// and order as dgrad_small_kernel (bit-identical).  Cout % 4 == 0, Cout <= 32, Gc, Goff % 4 == 0.
+constexpr int DC1_MAXC = 32;
+__global__ __launch_bounds__(256) void dgrad_c1_kernel(const float *G, int Gc, int Goff, const float *W, int Cout,
+                                                       float *dX, int B, int H, int Wd) {
+    __shared__ float4 gs[18 * 18 * (DC1_MAXC + 4) / 4];
+    const int tilesx = (Wd + 15) / 16, tilesy = (H + 15) / 16;
+    const int b = blockIdx.x / (tilesx * tilesy), t2 = blockIdx.x - b * tilesx * tilesy;
+    const int y0 = (t2 / tilesx) * 16, x0 = (t2 % tilesx) * 16;
+    const int ps = (Cout + 4) / 4;                              // pixel stride in float4
+    const int cq = Cout / 4;
+    for (int i = threadIdx.x; i < 18 * 18 * cq; i += 256) {
+        const int q = i % cq, px = i / cq, ly = px / 18, lx = px - ly * 18;
+        const int gy = min(max(y0 - 1 + ly, 0), H - 1), gx = min(max(x0 - 1 + lx, 0), Wd - 1);
+        gs[px * ps + q] = *reinterpret_cast<const float4 *>(G + (((size_t)b * H + gy) * Wd + gx) * Gc + Goff + 4 * q);
+    }
+    __syncthreads();
+    const int y = y0 + (threadIdx.x >> 4), x = x0 + (threadIdx.x & 15);
+    if (y >= H || x >= Wd) return;
+    int Py[6], Ty[6], Px[6], Tx[6];
+    const int ny = refl_taps(y, H, H, 1, Py, Ty), nx = refl_taps(x, Wd, Wd, 1, Px, Tx);
+    float s = 0.0f;
+    for (int i = 0; i < ny; ++i)
+        for (int j = 0; j < nx; ++j) {
+            const float4 *g = gs + ((Py[i] - y0 + 1) * 18 + (Px[j] - x0 + 1)) * ps;
+            const int t = Ty[i] * 3 + Tx[j];
+            for (int co = 0; co < Cout; co += 4) {
+                const float4 gv = g[co >> 2];
+                const float *wp = W + (size_t)co * 9 + t;
+                s = fmaf(gv.x, wp[0], fmaf(gv.y, wp[9], fmaf(gv.z, wp[18], fmaf(gv.w, wp[27], s))));
+            }
+        }
+    dX[((size_t)b * H + y) * Wd + x] = s;
+}
+
 // W [Cout][Cin][9] -> WT [9][Cout][Cin] (the layout dgrad_vec_kernel reads as float4 along Cin)
 __global__ void transpose_w_kernel(const float *W, int Cout, int Cin, float *WT) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
