@@ -64,7 +64,9 @@ def parse():
     p.add_argument("--graph", choices=["auto", "on", "off"], default="auto",
                    help="timed region: the whole L-frame recurrence replayed as one hipGraph "
                         "(v2e2v_amd/sequence.py) or the eager per-frame module calls; auto = both "
-                        "measured, the faster reported (the other in 'eager_vs_graph')")
+                        "measured, the graph replay reported as the headline (fixed, not the "
+                        "faster of two noisy timings), the eager time beside it in "
+                        "'eager_vs_graph'")
     p.add_argument("--sweep", default="1,8,32,64,128",
                    help="batch sizes of the small-batch / latency sweep (empty: skip)")
     p.add_argument("--cpu-frames", type=int, default=15,
@@ -101,7 +103,7 @@ def v2e2v_main(args, torch, vd, rank, world, device):
     cfgs = types.SimpleNamespace(event_mode="voxel_grid", num_bins=args.num_bins, pl=1.0, ps=1.0, ql=1.0, qs=1.0,
                                  C=0.2, threshold_sigma=0.03, cutoff_hz=30.0, refractory_period_s=0.001,
                                  base_channels=args.base_channels, depth=args.depth)
-    net = V2E2VNet(cfgs, [H, W], device)
+    net = V2E2VNet(cfgs, [H, W], device, lazy_count=True)    # no host sync per pack
     he_init_(torch, net.e2v_net, seed=7)
     net = net.to(device).eval()
     # synthetic HFR video resident in HBM: a textured background panning + a moving bright blob
@@ -533,9 +535,10 @@ def main():
         if args.graph in ("auto", "on"):
             seq = CistaSequence(model, vox)
             timings["graph"] = time_steps(torch, lambda: seq.run()[0][-1], args.steps, args.warmup, vd, device)
-    # the same choice on every rank: the max over ranks of each path, then the faster path
+    # the max over ranks of each path; the headline is the graph replay whenever it was timed
+    # (a fixed choice: taking the faster of two short timings would bias the metric upwards)
     el = {k: vd.max_over_ranks(v[0], device) for k, v in timings.items()}
-    path = min(el, key=el.get)
+    path = "graph" if "graph" in el else "eager"
     elapsed = el[path]
     rec = timings[path][1]
     rec = rec[0] if isinstance(rec, tuple) else rec

@@ -42,7 +42,7 @@
 extern "C" {
 #endif
 
-#define CISTA_ABI_VERSION 2
+#define CISTA_ABI_VERSION 3
 
 enum {
     CISTA_OK = 0,
@@ -106,13 +106,11 @@ int    cista_pack_params(const cista_config *cfg, const cista_params *params, vo
 /* scratch needed by cista_forward / the stage entries for one (B, H, W) */
 size_t cista_workspace_bytes(const cista_config *cfg, int B, int H, int W);
 
-/* Range flag.  The first int32 of every workspace (inference, training) is a sticky flag
- * that the kernels set to 1 when an activation they split into fp16 hi/lo parts has
- * |x| >= 65504 (or is inf): such a frame is not fp32-faithful.  The library never clears or
- * reads it (no host sync): the caller zeroes it when it allocates the workspace (and after
- * handling a report) and reads it asynchronously when it wants.  workspace bytes [0, 256)
- * are reserved for it. */
-#define CISTA_RANGE_FLAG_OFFSET 0
+/* Range.  The split-fp16 MFMA path has no range limit a caller must respect: a conv tile whose
+ * input holds a value the fp16 hi part cannot (|x| >= 65520) is recomputed in the same launch
+ * with its inputs pre-scaled by a power of two.  Workspace bytes [0, 256)
+ * stay reserved (ABI versions <= 2 kept a range flag there); nothing is written to them. */
+#define CISTA_WORKSPACE_RESERVED_BYTES 256
 
 /* one recurrent frame for B independent sequences */
 int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int W,
@@ -125,12 +123,15 @@ int cista_forward(const cista_config *cfg, const void *packed, int B, int H, int
  * replay it).  Frame f reads io[f] and must have the buffers cista_forward would; the recurrent
  * chaining is the caller's choice of pointers (io[f+1]'s prev pointers = io[f]'s outputs).
  * Every pointer is baked into the graph: replays recompute on whatever those buffers hold.
- * The parameters must be packed (and stay packed) before capture.  cista_sequence_launch
- * enqueues one replay on `stream`; cista_sequence_destroy frees the graph. */
+ * The parameters must be packed (and stay packed) before capture.  Capture runs frame 0 once,
+ * eagerly, on its private stream before recording (one-time kernel attributes, argument errors):
+ * that stream first waits for the work already enqueued on `stream` (an event), so inputs and
+ * parameters produced there are ready; the call returns after that frame has finished.
+ * cista_sequence_launch enqueues one replay on `stream`; cista_sequence_destroy frees the graph. */
 typedef struct cista_sequence cista_sequence;
 int  cista_sequence_capture(const cista_config *cfg, const void *packed, int B, int H, int W,
                             const cista_frame_io *io, int n_frames, void *workspace,
-                            size_t workspace_bytes, cista_sequence **out);
+                            size_t workspace_bytes, cista_sequence **out, void *stream);
 int  cista_sequence_launch(cista_sequence *seq, void *stream);
 void cista_sequence_destroy(cista_sequence *seq);
 
@@ -208,8 +209,8 @@ typedef struct {
     float *g_z_prev;           /* out (B,h,w,2C)                                    */
     float *g_h_prev;           /* out (B,h,w,C)                                     */
     float *g_c_prev;           /* out (B,h,w,C)                                     */
-    float *g_events;           /* out (B,nb,H,W) NCHW; NULL = not needed (appended: */
-                               /* ABI version 2)                                    */
+    float *g_events;           /* out (B,nb,H,W) NCHW; NULL = not needed (appended in */
+                               /* ABI version 2: read only when grads_bytes covers it) */
 } cista_grad_io;
 
 /* parameter gradients, same fields / layouts as cista_params; written (not accumulated) */
@@ -220,10 +221,13 @@ typedef struct {
     float *Dg_w, *Dg_b, *lstm_w, *lstm_b, *up_w, *up_b, *final_w, *final_b;
 } cista_param_grads;
 
+/* grads_bytes = sizeof(cista_grad_io) as the caller compiled it: members beyond it (fields
+ * appended by later ABI versions) are treated as NULL, never read. */
 int cista_backward(const cista_config *cfg, const void *packed, const cista_params *params,
                    int B, int H, int W, const cista_frame_io *io, const void *saved,
-                   size_t saved_bytes, const cista_grad_io *grads, const cista_param_grads *pgrads,
-                   void *workspace, size_t workspace_bytes, void *stream);
+                   size_t saved_bytes, const cista_grad_io *grads, size_t grads_bytes,
+                   const cista_param_grads *pgrads, void *workspace, size_t workspace_bytes,
+                   void *stream);
 
 #ifdef __cplusplus
 }

@@ -7,7 +7,7 @@ ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test failures,
 for step in "$@"; do
   case "$step" in
     tests)
-      timeout -k 10 600 python -m pytest tests -m gpu -q -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -p no:cacheprovider --timeout 300 --timeout-method thread ${TEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
       rc=$?; echo "tests rc=$rc"; tail -3 gpurun_out/gpu_tests.log; ok $rc || exit $rc ;;
     smoke)
       timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1

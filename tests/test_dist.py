@@ -58,3 +58,94 @@ def test_shard_partition_properties():
             flat = [i for p in parts for i in p]
             assert flat == list(range(n))
             assert max(map(len, parts)) - min(map(len, parts)) <= 1
+
+
+# ------------------------------------------------------------------ c4's data path
+TINY = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "train_tiny")
+
+
+def _tiny_dataset():
+    import types
+    from v2e2v_amd import data
+    cfgs = types.SimpleNamespace(path_to_train_data=TINY, num_bins=5, image_dim=[24, 32], num_events=300,
+                                 len_sequence=6, add_noise=False)
+    return data.TrainFixNEventData(os.path.join(TINY, "train_e2v.txt"), cfgs)
+
+
+def _seq_of(ds, events):
+    """Sequence index of a raw item: its first event's time is the line number of its first line
+    (tests/golden/make_train_tiny.py)."""
+    first_line = int(round(float(events[0, 0])))
+    return [s[0][0] for s in ds.sequence_line_id].index(first_line)
+
+
+def _loader_worker(rank, world, port, q):
+    os.environ.update(RANK=str(rank), WORLD_SIZE=str(world), LOCAL_RANK=str(rank),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    from v2e2v_amd import data
+    vd.init("gloo")
+    ds = _tiny_dataset()
+    res = {}
+    # per-rank batch 1: the rank's shard through the DataLoader (raw items; the GPU voxelisation
+    # of GpuVoxelLoader.__iter__ is not run on CPU), rank and world from the process group
+    ld = data.GpuVoxelLoader(ds, "cpu", batch_size=1)
+    res["world"] = (ld.rank, ld.world_size, len(ld))
+    res["plain"] = [_seq_of(ds, it[0][0]) for it in ld.loader]
+    ld = data.GpuVoxelLoader(ds, "cpu", batch_size=1, shuffle=True, seed=5)
+    for ep in (0, 1):
+        ld.set_epoch(ep)
+        res[f"shuf{ep}"] = [_seq_of(ds, it[0][0]) for it in ld.loader]
+    # per-rank batch 2: rank 0's first batch pairs a 6-frame and a 5-frame sequence -> refused
+    ld = data.GpuVoxelLoader(ds, "cpu", batch_size=2)
+    try:
+        next(iter(ld))
+        res["ragged"] = "accepted"
+    except RuntimeError as e:
+        res["ragged"] = "refused" if "equal size" in str(e) else repr(e)
+    gathered = [None] * world
+    torch.distributed.all_gather_object(gathered, res)
+    q.put((rank, gathered))
+    torch.distributed.destroy_process_group()
+
+
+def test_gloo_loader_shards_are_disjoint_and_cover_the_split():
+    world = 2
+    ds = _tiny_dataset()
+    assert len(ds) == 6 and sorted({len(s) for s in ds.sequence_line_id}) == [5, 6]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_loader_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=180) for _ in procs]
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    g = res[0][1]
+    assert [r["world"] for r in g] == [(0, 2, 3), (1, 2, 3)]
+    for key in ("plain", "shuf0", "shuf1"):
+        shards = [set(r[key]) for r in g]
+        assert all(len(r[key]) == 3 for r in g)                 # same step count on every rank
+        assert not (shards[0] & shards[1])                       # disjoint
+        assert shards[0] | shards[1] == set(range(6))            # together the whole split
+    assert g[0]["plain"] == [0, 2, 4] and g[1]["plain"] == [1, 3, 5]
+    assert g[0]["shuf0"] != g[0]["shuf1"] or g[1]["shuf0"] != g[1]["shuf1"]   # reshuffled per epoch
+    assert g[0]["ragged"] == "refused"                           # sequences 0 (6 frames) + 2 (5 frames)
+
+
+def test_sequence_shard_sampler_properties():
+    from v2e2v_amd.data import SequenceShardSampler
+    for n in (0, 1, 6, 7, 64, 65):
+        for w in (1, 2, 3, 8):
+            for shuffle in (False, True):
+                parts = []
+                for r in range(w):
+                    s = SequenceShardSampler(n, r, w, shuffle=shuffle, seed=1)
+                    s.set_epoch(3)
+                    parts.append(list(s))
+                    assert len(parts[-1]) == len(s) == n // w
+                flat = [i for p in parts for i in p]
+                assert len(flat) == len(set(flat)) == (n // w) * w and set(flat) <= set(range(n))
+    with pytest.raises(ValueError):
+        SequenceShardSampler(4, 2, 2)

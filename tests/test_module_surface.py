@@ -19,7 +19,7 @@ def test_library_exports_every_header_symbol():
     assert len(names) >= 11
     for n in names:
         assert hasattr(L, n), n
-    assert L.cista_abi_version() == 2
+    assert L.cista_abi_version() == 3
     for s in range(6):
         assert L.cista_status_string(s)
 
@@ -41,6 +41,15 @@ def test_sizes_and_invalid_config():
     assert L.cista_layer_fused(ctypes.byref(cfg), W0) == 1
     assert L.cista_layer_fused(ctypes.byref(cfg), IN) == 0
     assert L.cista_layer_fused(ctypes.byref(_lib.CistaConfig(64, 5, 9)), W0) == 0
+    # cista_backward reads only the cista_grad_io members the caller's struct has: a struct
+    # shorter than the ABI-1 fields is refused before any device work
+    fake = ctypes.c_void_p(256)
+    prm = _lib.CistaParams(*([256] * 25))
+    pg = _lib.CistaParamGrads(*([256] * 25))
+    gio = _lib.CistaGradIO()
+    saved = L.cista_saved_bytes(ctypes.byref(cfg), 1, 64, 64)
+    assert L.cista_backward(ctypes.byref(cfg), fake, ctypes.byref(prm), 1, 64, 64, ctypes.byref(io), fake, saved,
+                            ctypes.byref(gio), 16, ctypes.byref(pg), fake, 1 << 40, None) == 1
     odd = _lib.CistaConfig(48, 5, 5)   # base_channels % 32 != 0 -> unsupported, not wrong
     assert L.cista_forward(ctypes.byref(odd), ctypes.c_void_p(1), 1, 64, 64,
                            ctypes.byref(io), None, 0, None) == 2

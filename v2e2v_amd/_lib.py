@@ -97,12 +97,12 @@ def _declare(lib):
         "cista_forward_train": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO),
                                         c_void_p, c_size_t, c_void_p, c_size_t, c_void_p]),
         "cista_backward": (c_int, [P(CistaConfig), c_void_p, P(CistaParams), c_int, c_int, c_int,
-                                   P(CistaFrameIO), c_void_p, c_size_t, P(CistaGradIO),
+                                   P(CistaFrameIO), c_void_p, c_size_t, P(CistaGradIO), c_size_t,
                                    P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
         "cista_sequence_capture": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO), c_int,
-                                           c_void_p, c_size_t, P(c_void_p)]),
+                                           c_void_p, c_size_t, P(c_void_p), c_void_p]),
         "cista_sequence_launch": (c_int, [c_void_p, c_void_p]),
         "cista_sequence_destroy": (None, [c_void_p]),
         # include/cista_voxel.h

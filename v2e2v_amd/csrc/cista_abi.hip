@@ -106,7 +106,6 @@ struct Workspace {
     float *x1;     // (B,h,w,C)
     float *z0;     // (B,h,w,2C)
     float *xb;     // (B,h,w,C): ISTA x = x1 - D(z); later Dg output y
-    int *rflag;    // bytes [0, 4): the range flag (include/cista_lstc.h), caller-owned
     size_t bytes;
 };
 
@@ -119,7 +118,6 @@ Workspace carve(void *ws, int B, int H, int W, int C) {
     Workspace w;
     size_t off = WS_HEADER;
     char *base = static_cast<char *>(ws);
-    w.rflag = reinterpret_cast<int *>(base);
     w.full = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * H * W * C * 4);
     w.x1 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * C * 4);
     w.z0 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * 2 * C * 4);
@@ -242,7 +240,11 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 ? 4 : 1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
     if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
     const size_t epi_lds = (size_t)4 * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
-    hipLaunchKernelGGL(kern, grid, dim3(256), t.lds > epi_lds ? t.lds : epi_lds, st, a);
+    // + 8 words of range-pass scratch right after the epilogue's LDS (inside the dead staging
+    // images when those are larger)
+    a.lds_flag = (int)(epi_lds / 4);
+    const size_t lds = t.lds > epi_lds + 32 ? t.lds : epi_lds + 32;
+    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
 
@@ -394,7 +396,6 @@ struct Frame {
     float *lg;             // ConvLSTM gates (i, r, o, g) post-activation (B,h,w,4C)
     float *u;              // relu(upsamp_conv(...))                      (B,H,W,C)
     bool need_full;        // the input stage must write x_full (the backward's recompute)
-    int *rflag;            // range flag (workspace header)
     hipStream_t st;
 };
 
@@ -433,7 +434,6 @@ inline bool up4_path(int C) { return CISTA_UP4 && C == 64; }
 ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int Hout, int Wout,
                      const float *in0, int c0, const float *in1, int c1) {
     ConvArgs a = conv_args(f.packed, f.L, id, C, B, Hin, Win, Hout, Wout, in0, c0, in1, c1);
-    a.rflag = f.rflag;
     return a;
 }
 
@@ -645,7 +645,7 @@ Frame make_frame(const cista_config *cfg, const void *packed, int B, int H, int 
     f.cfg = cfg; f.packed = packed; f.L = make_layout(*cfg);
     f.B = B; f.H = H; f.W = W; f.h = H / 2; f.w = W / 2; f.C = cfg->base_channels;
     const Workspace wsp = carve(ws, B, H, W, f.C);
-    f.full = wsp.full; f.x1 = wsp.x1; f.z0 = wsp.z0; f.xb = wsp.xb; f.rflag = wsp.rflag;
+    f.full = wsp.full; f.x1 = wsp.x1; f.z0 = wsp.z0; f.xb = wsp.xb;
     f.st = static_cast<hipStream_t>(stream);
     return f;
 }
@@ -1333,14 +1333,22 @@ struct cista_sequence {
 
 int cista_sequence_capture(const cista_config *cfg, const void *packed, int B, int H, int W,
                            const cista_frame_io *io, int n_frames, void *workspace, size_t workspace_bytes,
-                           cista_sequence **out) {
+                           cista_sequence **out, void *stream) {
     if (!out || !io || n_frames <= 0) return CISTA_ERR_INVALID;
     *out = nullptr;
     hipStream_t cs;
     if (hipStreamCreateWithFlags(&cs, hipStreamNonBlocking) != hipSuccess) return CISTA_ERR_HIP;
+    // the private stream starts after the work the caller has enqueued on `stream` (inputs,
+    // packed parameters, the workspace's previous users)
+    int status = CISTA_OK;
+    hipEvent_t ready = nullptr;
+    if (hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(ready, static_cast<hipStream_t>(stream)) != hipSuccess ||
+        hipStreamWaitEvent(cs, ready, 0) != hipSuccess)
+        status = CISTA_ERR_HIP;
     // a first eager frame on the private stream: one-time kernel attributes (LDS limits) are set
     // outside the capture, and argument errors surface before any graph exists
-    int status = cista_forward(cfg, packed, B, H, W, &io[0], workspace, workspace_bytes, cs);
+    if (status == CISTA_OK) status = cista_forward(cfg, packed, B, H, W, &io[0], workspace, workspace_bytes, cs);
     if (status == CISTA_OK && hipStreamSynchronize(cs) != hipSuccess) status = CISTA_ERR_HIP;
     hipGraph_t g = nullptr;
     if (status == CISTA_OK) {
@@ -1353,6 +1361,7 @@ int cista_sequence_capture(const cista_config *cfg, const void *packed, int B, i
     hipGraphExec_t ex = nullptr;
     if (status == CISTA_OK && hipGraphInstantiate(&ex, g, nullptr, nullptr, 0) != hipSuccess) status = CISTA_ERR_HIP;
     (void)hipStreamDestroy(cs);
+    if (ready) (void)hipEventDestroy(ready);
     if (status != CISTA_OK) {
         if (g) (void)hipGraphDestroy(g);
         return status;
@@ -1499,8 +1508,8 @@ int cista_forward_train(const cista_config *cfg, const void *packed, int B, int 
 
 int cista_backward(const cista_config *cfg, const void *packed, const cista_params *params, int B,
                    int H, int W, const cista_frame_io *io, const void *saved, size_t saved_bytes,
-                   const cista_grad_io *grads, const cista_param_grads *pg, void *workspace,
-                   size_t workspace_bytes, void *stream) {
+                   const cista_grad_io *grads, size_t grads_bytes, const cista_param_grads *pg,
+                   void *workspace, size_t workspace_bytes, void *stream) {
     CHECK(check_common(cfg, packed, B, H, W));
     CHECK(train_supported(cfg));
     if (!params || !io || !saved || !grads || !pg || !workspace) return CISTA_ERR_INVALID;
@@ -1514,6 +1523,11 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     if ((H & 1) || (W & 1) || H < 4 || W < 4) return CISTA_ERR_INVALID;
     const Saved sv = carve_saved(const_cast<void *>(saved), *cfg, B, H, W);
     if (saved_bytes < sv.bytes) return CISTA_ERR_WORKSPACE;
+    // the caller's view of cista_grad_io: members it does not have are NULL (never read)
+    constexpr size_t GIO_V1 = offsetof(cista_grad_io, g_events);
+    if (grads_bytes < GIO_V1) return CISTA_ERR_INVALID;
+    cista_grad_io g = {};
+    memcpy(&g, grads, grads_bytes < sizeof(g) ? grads_bytes : sizeof(g));
     Bwd k;
     k.cfg = cfg; k.packed = packed; k.L = make_layout(*cfg);
     k.B = B; k.H = H; k.W = W; k.h = H / 2; k.w = W / 2; k.C = cfg->base_channels;
@@ -1523,6 +1537,6 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     // the gradient-scale slots {amax, ticket} start at zero (absmax_scale_kernel re-zeroes them)
     if (hipMemsetAsync(k.ws.amax, 0, 8 * sizeof(unsigned), k.st) != hipSuccess) return CISTA_ERR_HIP;
-    return run_backward(k, *params, *io, sv, *grads, *pg);
+    return run_backward(k, *params, *io, sv, g, *pg);
 }
 }  // extern "C"

@@ -58,6 +58,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_RANGE_CHECK
 #define CISTA_RANGE_CHECK 1
 #endif
+#ifndef CISTA_RERUN
+#define CISTA_RERUN 1
+#endif
 // A/B switches: CISTA_PRIO=1 raises the wave priority around each tap's MFMA cluster;
 // CISTA_NT=1 makes the epilogue's burst stores non-temporal
 #ifndef CISTA_PRIO
@@ -148,7 +151,8 @@ struct ConvArgs {
     //   4*Cout channels in the reference gate order; EPI_UP_Q: out1 = u = relu(acc + b)
     float *out2;
     const float *ascale; // optional [2]: {s, 1/s} power-of-two input pre-scale (dgrad inputs)
-    int *rflag;          // optional: set to 1 when a staged |x| >= 65504 (fp16 split range)
+    int lds_flag;        // 4-byte LDS index of 8 words of range-pass scratch, outside the epilogue's
+                         // LDS (the host sizes the allocation for it)
     int border;          // 0, or the border-strip tiling (see the kernel's tile origin)
     // STAGE_S2D: in0 = events (B, s2d_nb, 2Hin, 2Win), s2d_img = prev image (B, 1, 2Hin, 2Win)
     const float *s2d_img;
@@ -359,6 +363,30 @@ __device__ __forceinline__ void stage_commit(u32x4 *buf, int HPpad, const float4
     }
 }
 
+// range pass helpers (rare path): max |x| of 8 staged values (fmaxf drops NaN), and of one
+// K-chunk's halo items of the single-buffered loop
+__device__ __forceinline__ float absmax8(const float4 &a, const float4 &b) {
+    const float m0 = fmaxf(fmaxf(fabsf(a.x), fabsf(a.y)), fmaxf(fabsf(a.z), fabsf(a.w)));
+    const float m1 = fmaxf(fmaxf(fabsf(b.x), fabsf(b.y)), fmaxf(fabsf(b.z), fabsf(b.w)));
+    return fmaxf(m0, m1);
+}
+
+template <int STAGE>
+__device__ float stage_absmax(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd, const float *seg,
+                              int segC, int choff) {
+    const int HP = HH * HWd;
+    const int nitems = ((HP + 7) & ~7) * 4;
+    float mx = 0.0f;
+    for (int it = threadIdx.x; it < nitems; it += 256) {
+        const int hp = ((it >> 5) << 3) | (it & 7);
+        if (hp >= HP) continue;
+        float4 v0, v1;
+        stage_load<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, (it >> 3) & 3, v0, v1);
+        mx = fmaxf(mx, absmax8(v0, v1));
+    }
+    return mx;
+}
+
 // Per-thread halo items of the double-buffered loop are the same (hp, g) for every K-chunk, so
 // their source pixel (reflect / zero padding resolved) is computed once per tile; a chunk's
 // load address is then seg + pixel * segC + choff + 8 g in 32-bit arithmetic.
@@ -475,6 +503,127 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
     }
 }
 
+// Range pass, rare path (see conv3x3_split3): some staged value of this tile did not fit the
+// fp16 hi part.  The tile scans its inputs for max |x| (every K-chunk), takes the power of two s
+// with max |x s| <= 16384, and recomputes its accumulators from scratch on the same split-f16
+// MFMAs with every staged value pre-scaled by s (exact); the epilogue divides s out.  Accuracy is
+// the split path's relative to the tile's largest input.  A plain single-buffered K loop (one
+// LDS image, no prefetch) that recomputes every address per tap, so that nothing is held across
+// it: ~60 VGPRs beside the accumulators, which keeps the main loop's allocation (a second trip
+// through the main loop spilled 15-45 VGPRs in the 256-VGPR convs).  An fp32-MFMA re-run
+// (v_mfma_f32_16x16x4f32 over the unsplit inputs) was tried first: its 432-step sequential fp32
+// sums were 3-11x less accurate than ATen's blocked sums on saturating gate convs.
+// packed output column (gate-interleaved n-tiles, pack_conv_kernel) -> reference output channel
+__device__ __forceinline__ int packed_col_to_cout(int pc, int N, int G) {
+    const int nt = pc >> 4, r = pc & 15;
+    const int g = nt % G, cblk = nt / G;
+    return g * (N / G) + cblk * 16 + r;
+}
+
+template <int STAGE>
+__device__ __forceinline__ void rare_item(const ConvArgs &a, int b, int iy0, int ix0, int HWd, const float *seg,
+                                          int segC, int choff, int hp, int g, float4 &v0, float4 &v1) {
+    if constexpr (STAGE == STAGE_CLAMP || STAGE == STAGE_S2D) {
+        const int hy = hp / HWd, hx = hp - hy * HWd;
+        const int iy = min(max(iy0 + hy, 0), a.Hin - 1), ix = min(max(ix0 + hx, 0), a.Win - 1);
+        int sp[1], sgg[1] = {g};
+        sp[0] = STAGE == STAGE_CLAMP ? (b * a.Hin + iy) * a.Win + ix : (2 * iy) * (2 * a.Win) + 2 * ix;
+        float4 w0[1], w1[1];
+        stage_issue_px<STAGE, 1>(a, seg, segC, choff, sp, sgg, w0, w1, b);
+        v0 = w0[0];
+        v1 = w1[0];
+    } else {
+        stage_load<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, g, v0, v1);
+    }
+}
+
+template <int MT_W, int WM, int NW, int STAGE>
+__device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32x4 (&acc)[MT_W][NW], int b, int oy0,
+                                             int ox0, int wm, int nt0, int nchunks, int kc0) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int S = (STAGE == STAGE_S2) ? 2 : 1;
+    const int HWd = (a.TW - 1) * S + 3, HH = (a.TH - 1) * S + 3;
+    const int HP = HH * HWd;
+    const int HPpad = (HP + 15) & ~15;
+    const int iy0 = STAGE == STAGE_ZP2 ? oy0 - 2 : oy0 * S - 1;
+    const int ix0 = STAGE == STAGE_ZP2 ? ox0 - 2 : ox0 * S - 1;
+    const int nitems = ((HP + 7) & ~7) * 4;
+    const size_t tapstride = (size_t)(a.N >> 4) * 2 * 64;
+    auto seg_of = [&](int kc, const float *&seg, int &segC, int &choff) {
+        seg = kc < kc0 ? a.in0 : a.in1;
+        segC = kc < kc0 ? a.c0 : a.c1;
+        choff = (kc < kc0 ? kc : kc - kc0) * 32;
+    };
+    float mx = 0.0f;
+    for (int kc = 0; kc < nchunks; ++kc) {
+        const float *seg; int segC, choff;
+        seg_of(kc, seg, segC, choff);
+        for (int it = threadIdx.x; it < nitems; it += 256) {
+            const int hp = ((it >> 5) << 3) | (it & 7);
+            if (hp >= HP) continue;
+            float4 v0, v1;
+            rare_item<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, (it >> 3) & 3, v0, v1);
+            mx = fmaxf(mx, absmax8(v0, v1));
+        }
+    }
+    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    float *flm = reinterpret_cast<float *>(smem) + a.lds_flag + 4;
+    if (lane == 0) flm[wave] = mx;
+    __syncthreads();
+    mx = fmaxf(fmaxf(flm[0], flm[1]), fmaxf(flm[2], flm[3]));
+    if (!(mx < 3.0e38f)) return 1.0f;                   // an inf input: the reference gives inf / NaN too
+    int e = (int)floorf(log2f(16384.0f / mx));
+    e = e < -126 ? -126 : (e > 0 ? 0 : e);
+    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ldexpf(1.0f, e))));
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+        for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
+    f16x2 unused = {};
+    for (int kc = 0; kc < nchunks; ++kc) {
+        const float *seg; int segC, choff;
+        seg_of(kc, seg, segC, choff);
+        __syncthreads();                                // the maxima / previous chunk's reads are done
+        for (int it = threadIdx.x; it < nitems; it += 256) {
+            const int hp = ((it >> 5) << 3) | (it & 7), g = (it >> 3) & 3;
+            if (hp >= HP) continue;
+            float4 v0, v1;
+            rare_item<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, g, v0, v1);
+            v0.x *= s; v0.y *= s; v0.z *= s; v0.w *= s;
+            v1.x *= s; v1.y *= s; v1.z *= s; v1.w *= s;
+            u32x4 hi, lo;
+            split8(v0, v1, hi, lo, unused);
+            smem[g * HPpad + hp] = hi;
+            smem[(4 + g) * HPpad + hp] = lo;
+        }
+        __syncthreads();
+#pragma unroll 1
+        for (int tap = 0; tap < 9; ++tap) {
+            // opaque lane id: the per-m-tile A addresses are recomputed every tap instead of being
+            // hoisted out of the loops and held (which spilled the main loop's registers)
+            int ln = lane;
+            asm volatile("" : "+v"(ln));
+            int abase[MT_W];
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) {
+                int py, px;
+                tile_pixel(a, (wm * MT_W + m) * 16 + (ln & 15), py, px);
+                abase[m] = (ln >> 4) * HPpad + py * S * HWd + px * S;
+            }
+            const u32x4 *wq = a.wpack + ((size_t)kc * 9 + tap) * tapstride + (size_t)nt0 * 128 + ln;
+            u32x4 bh[NW], bl[NW];
+#pragma unroll
+            for (int n = 0; n < NW; ++n) {
+                bh[n] = wq[n * 128];
+                bl[n] = wq[n * 128 + 64];
+            }
+            mfma_tap<MT_W, NW>(acc, smem, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
+        }
+    }
+    __syncthreads();                                    // the epilogue may reuse the LDS
+    return s;
+}
+
 // ------------------------------------------------------------------------------------------
 // The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
 // MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
@@ -559,7 +708,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-    f16x2 amax = {};     // running max of the staged |hi| parts (range flag, see ConvArgs.rflag)
+    f16x2 amax = {};     // running max of the staged |hi| parts (the range pass below)
     const int NT = a.N >> 4;
     const int nt0 = (nblk * WN + wn) * NW;
     const int kc0 = a.c0 >> 5;
@@ -571,6 +720,15 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         segC = kc < kc0 ? a.c0 : a.c1;
         choff = (kc < kc0 ? kc : kc - kc0) * 32;
     };
+    float insc = 1.0f;   // the range pass's input pre-scale (1 unless the tile was re-run)
+    // Range pass.  A staged value whose fp16 hi part overflows (|x| >= 65520, far beyond what
+    // the reference's activations reach on normalised voxels, but legal fp32) would make the
+    // split products wrong.  The staging keeps a packed running max of |hi| (4 v_pk_max_f16 per 8
+    // values); after the K loop the workgroup ORs the overflow bits (one barrier per tile) and,
+    // only if one is set, recomputes its accumulators with pre-scaled inputs (range_rerun).
+    // Nothing is reported late and no frame is refused: the tile is simply right.  (A second
+    // trip through the main loop instead -- an outer loop, or a pre-scaled split re-run -- made
+    // the compiler spill 15-45 VGPRs in the 256-VGPR convs.)
     if constexpr (NI > 0) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
         // B prefetch depth: deep where the accumulators leave room (the 6 x 2-tile waves)
@@ -638,7 +796,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
             __syncthreads();
             if (kc < 8) CISTA_STAMP(3 + kc, __builtin_amdgcn_s_memtime());
         }
-    } else
+    } else {
     for (int kc = 0; kc < nchunks; ++kc) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
@@ -692,12 +850,20 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
             }
         }
     }
+        __syncthreads();               // the last chunk's A-fragment reads are done (LDS reuse)
+    }
 
     CISTA_STAMP(11, __builtin_amdgcn_s_memtime());
-    // an activation beyond the fp16 range of the hi part (or inf): the result is not fp32-faithful
-    if (CISTA_RANGE_CHECK && a.rflag) {
-        const _Float16 m = amax[0] > amax[1] ? amax[0] : amax[1];
-        if (__builtin_isinf((float)m)) *a.rflag = 1;
+    if constexpr (CISTA_RANGE_CHECK) {
+        int *fl = reinterpret_cast<int *>(smem) + a.lds_flag;   // [0, 4): per-wave overflow bits
+        {
+            const _Float16 hm = amax[0] > amax[1] ? amax[0] : amax[1];
+            const bool wany = __ballot(__builtin_isinf((float)hm) ? 1 : 0) != 0;
+            if (lane == 0) fl[wave] = wany ? 1 : 0;
+        }
+        __syncthreads();
+        if (CISTA_RERUN && !a.ascale && (fl[0] | fl[1] | fl[2] | fl[3]) != 0)
+            insc = range_rerun<MT_W, WM, NW, STAGE>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0);
     }
 
     // ---------------------------------- epilogue ----------------------------------------
@@ -708,6 +874,13 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     for (int m = 0; m < MT_W; ++m)
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
+    if (__builtin_expect(insc != 1.0f, 0)) {           // the range pass's pre-scale, up to 2^126
+        const float iv = 1.0f / insc;                  // (a separate step: ws * iv may overflow)
+#pragma unroll
+        for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+            for (int n = 0; n < NW; ++n) acc[m][n] *= iv;
+    }
 
     if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE || EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE) {
         constexpr bool PH4 = EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE;
@@ -785,7 +958,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     // written to LDS as [pixel][column] and read back so that a lane owns 4 consecutive
     // channels of one pixel -> the aux reads and output writes are 16-byte, fully coalesced
     // (16 lanes = one pixel's 256-byte channel run) instead of 4-byte scattered accesses.
-    __syncthreads();                                       // staging LDS is free from here on
+    // the staging LDS is free from here on (the K loop / range pass ended with a barrier)
     constexpr int LDT = NW * 16 + 4;                       // padded row: conflict-free writes
     constexpr int CG = (NW / G) * 4;                       // 4-channel groups per pixel
     static_assert(64 % CG == 0, "a lane's channel group must be the same for every item");
@@ -1607,12 +1780,6 @@ struct PackArgs {
     float *bp;           // [N] packed-column bias
     int Cout, Cin, G;    // G: gates grouped per channel block
 };
-
-__device__ __forceinline__ int packed_col_to_cout(int pc, int N, int G) {
-    const int nt = pc >> 4, r = pc & 15;
-    const int g = nt % G, cblk = nt / G;
-    return g * (N / G) + cblk * 16 + r;
-}
 
 __global__ void pack_conv_kernel(const PackArgs a) {
     const int NT = a.Cout / 16;

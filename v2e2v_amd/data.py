@@ -13,6 +13,10 @@ the voxelisation they end in runs on the GPU through the batched HIP voxelizer
   touch the GPU) and ``GpuVoxelLoader`` turns a batch of them into exactly what the reference
   loader yields -- ``(seq_events, img, gt_img)`` with ``seq_events[s]`` a (B, num_bins, H, W)
   voxel tensor -- voxelised on the GPU (event_preprocess(filter_hot_pixel=False), :187-193).
+* ``SequenceShardSampler``     -- data-parallel training (config c4): the reference's
+  ``DataLoader(shuffle=cfgs.shuffle)`` (train_e2v.py:60-61) becomes one rank-disjoint shard of
+  the sequences per process; ``GpuVoxelLoader(..., rank, world_size)`` builds it (by default from
+  the initialised torch.distributed group), so ``batch_size`` is the PER-RANK batch.
 
 Images are read with PIL (the reference uses cv2.IMREAD_GRAYSCALE; cv2 is not installed):
 8-bit grayscale / 255, float32.
@@ -193,18 +197,74 @@ class TrainFixNEventData(torch.utils.data.Dataset):
         return torch.from_numpy(events), torch.from_numpy(sizes), torch.from_numpy(img), torch.from_numpy(gt)
 
 
+class SequenceShardSampler(torch.utils.data.Sampler):
+    """The sequences of one rank of a data-parallel job.  Every epoch the same permutation is
+    drawn on all ranks (torch.randperm seeded with seed + epoch when shuffle, else identity), cut
+    to a multiple of world_size, and rank r takes positions r, r + world, r + 2 world, ...: the
+    shards are disjoint, every rank yields the same number of sequences (so DDP ranks run the
+    same number of steps and meet in every gradient all-reduce), and together they cover the
+    epoch except its last n % world_size sequences (a different few each shuffled epoch).
+    Unlike torch's DistributedSampler no sequence is duplicated to pad the epoch."""
+
+    def __init__(self, n_sequences: int, rank: int, world_size: int, shuffle: bool = False, seed: int = 0):
+        if world_size < 1 or not 0 <= rank < world_size:
+            raise ValueError(f"rank {rank} outside world_size {world_size}")
+        self.n, self.rank, self.world = int(n_sequences), int(rank), int(world_size)
+        self.shuffle, self.seed, self.epoch = bool(shuffle), int(seed), 0
+
+    def set_epoch(self, epoch: int):
+        self.epoch = int(epoch)
+
+    def __iter__(self):
+        if self.shuffle:
+            g = torch.Generator().manual_seed(self.seed + self.epoch)
+            order = torch.randperm(self.n, generator=g).tolist()
+        else:
+            order = list(range(self.n))
+        used = (self.n // self.world) * self.world
+        return iter(order[self.rank:used:self.world])
+
+    def __len__(self):
+        return self.n // self.world
+
+
 class GpuVoxelLoader:
     """Iterate a DataLoader over TrainFixNEventData and voxelise each batch on the GPU:
     yields (seq_events, img, gt_img) like the reference loader (train_e2v.py:104-107), with every
     B x L window of the batch voxelised in one cista_voxelize call (mode 'std', no hot-pixel
     filter, train_data_loaders.py:192).  add_noise (``add_noise_to_voxel`` with std 0.1, fraction
-    1, :209-210) is applied on the device with torch's RNG, as the reference does with torch."""
+    1, :209-210) is applied on the device with torch's RNG, as the reference does with torch.
 
-    def __init__(self, dataset: TrainFixNEventData, device, **loader_kwargs):
+    Data parallel (config c4): with world_size > 1 -- given, or taken from the initialised
+    torch.distributed group -- the loader reads only this rank's SequenceShardSampler shard and
+    ``batch_size`` is the per-rank batch (global batch = world_size x batch_size).  ``shuffle``
+    then goes to the sampler (same permutation on every rank); call ``set_epoch`` each epoch."""
+
+    def __init__(self, dataset: TrainFixNEventData, device, rank: int | None = None, world_size: int | None = None,
+                 shuffle: bool = False, seed: int = 0, **loader_kwargs):
         self.ds = dataset
         self.device = torch.device(device)
+        if world_size is None:
+            dd = torch.distributed
+            world_size = dd.get_world_size() if dd.is_available() and dd.is_initialized() else 1
+            rank = dd.get_rank() if world_size > 1 else 0
+        self.rank, self.world_size = int(rank or 0), int(world_size)
+        self.sampler = None
+        if self.world_size > 1:
+            if "sampler" in loader_kwargs or loader_kwargs.get("shuffle"):
+                raise ValueError("data-parallel GpuVoxelLoader: pass shuffle=/seed= to the loader, not a sampler")
+            self.sampler = SequenceShardSampler(len(dataset), self.rank, self.world_size, shuffle, seed)
+            loader_kwargs["sampler"] = self.sampler
+        else:
+            loader_kwargs.setdefault("shuffle", shuffle)
         loader_kwargs.setdefault("collate_fn", self._collate)
         self.loader = torch.utils.data.DataLoader(dataset, **loader_kwargs)
+
+    def set_epoch(self, epoch: int):
+        """Reshuffle the rank shards for this epoch (no-op single-process: the DataLoader's own
+        shuffle draws a new order every epoch)."""
+        if self.sampler is not None:
+            self.sampler.set_epoch(epoch)
 
     @staticmethod
     def _collate(items):

@@ -63,10 +63,11 @@ class CistaSequence:
         self._ws = m.workspace(self.B, self.H, self.W, self.voxels.device)
         handle = ctypes.c_void_p()
         L = _lib.lib()
-        torch.cuda.current_stream(self.voxels.device).synchronize()     # inputs / packing done
+        # the library orders its capture stream after torch's current stream (inputs, packing)
         _lib.check(L.cista_sequence_capture(ctypes.byref(m._cfg()), self._packed.data_ptr(), self.B, self.H, self.W,
                                             self._io(), self.L, self._ws.data_ptr(), self._ws.numel(),
-                                            ctypes.byref(handle)), "cista_sequence_capture")
+                                            ctypes.byref(handle), _lib.stream_handle(self.voxels.device)),
+                   "cista_sequence_capture")
         self._seq = handle
 
     def run(self):
@@ -75,8 +76,6 @@ class CistaSequence:
             self._capture()
         dev = self.voxels.device
         _lib.check(_lib.lib().cista_sequence_launch(self._seq, _lib.stream_handle(dev)), "cista_sequence_launch")
-        if self.model.range_check:
-            self.model._range_poll(self._ws)
         last = self.sets[(self.L - 1) % 2]
         return self.recs, [last[0], last[1], (last[2], last[3])]
 

@@ -14,6 +14,7 @@ cv2 state display are not built (V2E2V never uses them).
 from __future__ import annotations
 
 import ctypes
+import numbers
 import random
 
 import numpy as np
@@ -34,10 +35,14 @@ class CistaV2EHostState(ctypes.Structure):
     _fields_ = [("initialized", ctypes.c_int), ("t_previous", ctypes.c_float), ("draw", ctypes.c_ulonglong)]
 
 
-class EventCount:
-    """The emulator's event count, kept on the device until it is read (the reference returns
-    a Python int, v2e_model.py:536; reading it per pack would be a host sync per pack).  Acts as
-    an int wherever one is used: int(), comparisons, arithmetic, formatting."""
+class EventCount(numbers.Integral):
+    """The emulator's event count kept on the device until it is read -- the opt-in
+    ``lazy_count=True`` mode of EventEmulator, for pipelines that must not host-sync once per pack
+    (the default returns a plain Python int, as the reference does, v2e_model.py:536).  A full
+    numbers.Integral: int(), operator.index, comparisons, hashing, arithmetic, //, %, **, bit
+    operations and formatting all act on the integer value (read once, on first use).  It is not
+    an ``int`` instance (an int's value is fixed when it is made, and this one is not known until
+    the GPU has run): ``isinstance(n, int)`` and json need ``int(n)``."""
 
     __slots__ = ("_t", "_v")
 
@@ -50,16 +55,51 @@ class EventCount:
             self._t = None
         return self._v
 
-    __index__ = __int__
+    def __index__(self):
+        return int(self)
 
     def __float__(self):
         return float(int(self))
 
+    def __complex__(self):
+        return complex(int(self))
+
+    def __bool__(self):
+        return int(self) != 0
+
+    def __hash__(self):
+        return hash(int(self))
+
+    def __repr__(self):
+        return repr(int(self))
+
+    __str__ = __repr__
+
+    def __format__(self, spec):
+        return format(int(self), spec)
+
+    def __round__(self, ndigits=None):
+        return int(self) if ndigits is None else round(int(self), ndigits)
+
+    def __trunc__(self):
+        return int(self)
+
+    def __floor__(self):
+        return int(self)
+
+    def __ceil__(self):
+        return int(self)
+
+    @property
+    def numerator(self):
+        return int(self)
+
+    @property
+    def denominator(self):
+        return 1
+
     def __eq__(self, o):
         return int(self) == o
-
-    def __ne__(self, o):
-        return int(self) != o
 
     def __lt__(self, o):
         return int(self) < o
@@ -73,38 +113,40 @@ class EventCount:
     def __ge__(self, o):
         return int(self) >= o
 
-    def __hash__(self):
-        return hash(int(self))
+    def __neg__(self):
+        return -int(self)
 
-    def __add__(self, o):
-        return int(self) + o
+    def __pos__(self):
+        return int(self)
 
-    __radd__ = __add__
+    def __abs__(self):
+        return abs(int(self))
 
-    def __mul__(self, o):
-        return int(self) * o
+    def __invert__(self):
+        return ~int(self)
 
-    __rmul__ = __mul__
+    def __pow__(self, o, mod=None):
+        return pow(int(self), o, mod)
 
-    def __sub__(self, o):
-        return int(self) - o
+    def __rpow__(self, o, mod=None):
+        return pow(o, int(self), mod)
 
-    def __rsub__(self, o):
-        return o - int(self)
 
-    def __truediv__(self, o):
-        return int(self) / o
+def _binop(name):
+    def fwd(self, o):
+        return getattr(int(self), name)(o)
 
-    def __bool__(self):
-        return int(self) != 0
+    def rev(self, o):
+        return getattr(int(self), "__r" + name[2:])(o)
+    return fwd, rev
 
-    def __repr__(self):
-        return repr(int(self))
 
-    __str__ = __repr__
-
-    def __format__(self, spec):
-        return format(int(self), spec)
+for _op in ("__add__", "__sub__", "__mul__", "__truediv__", "__floordiv__", "__mod__", "__divmod__",
+            "__lshift__", "__rshift__", "__and__", "__xor__", "__or__"):
+    _f, _r = _binop(_op)
+    setattr(EventCount, _op, _f)
+    setattr(EventCount, "__r" + _op[2:], _r)
+EventCount.__abstractmethods__ = frozenset()
 
 
 class EventEmulator(torch.nn.Module):
@@ -113,7 +155,7 @@ class EventEmulator(torch.nn.Module):
     def __init__(self, output_mode, pl=1, ps=1, ql=1, qs=1, num_bins=5, pos_thres=0.2, neg_thres=0.2,
                  sigma_thres=0.03, cutoff_hz=0, leak_rate_hz=0.1, refractory_period_s=0, shot_noise_rate_hz=0,
                  leak_jitter_fraction=0.1, noise_rate_cov_decades=0.1, seed=0, show_dvs_model_state=None,
-                 device="cuda"):
+                 device="cuda", lazy_count=False):
         super().__init__()
         if output_mode != "voxel_grid":
             raise NotImplementedError("only output_mode='voxel_grid' (the V2E2V mode) is built")
@@ -130,6 +172,7 @@ class EventEmulator(torch.nn.Module):
         self.num_events = 0
         self.frame_counter = 0
         self._shape = None
+        self.lazy_count = lazy_count   # True: num_events is an EventCount (no host sync per call)
 
     def reset(self):
         """v2e_model.py:255-263: the next forward re-initialises the base frame."""
@@ -162,15 +205,15 @@ class EventEmulator(torch.nn.Module):
         if status == 1 and self.hs.initialized:
             raise ValueError("this frame time must be later than previous frame time")   # :339-342
         _lib.check(status, "cista_v2e_forward")
-        # no host sync per pack: the count stays a device scalar until someone reads it
-        self.num_events = EventCount(nev)
+        # the reference returns a Python int; lazy_count keeps it on the device until it is read
+        self.num_events = EventCount(nev) if self.lazy_count else int(nev.item())
         return out, self.num_events
 
 
 class V2E2VNet(torch.nn.Module):
     """model_v2e2v.py:9-128: EventEmulator (voxel grid) -> CistaLSTCNet."""
 
-    def __init__(self, cfgs, image_dim, device):
+    def __init__(self, cfgs, image_dim, device, lazy_count=False):
         super().__init__()
         self.height, self.width = image_dim
         self.device = device
@@ -184,7 +227,7 @@ class V2E2VNet(torch.nn.Module):
                                      ql=cfgs.ql, qs=cfgs.qs, pos_thres=cfgs.C, neg_thres=cfgs.C,
                                      sigma_thres=cfgs.threshold_sigma, cutoff_hz=cfgs.cutoff_hz,
                                      refractory_period_s=cfgs.refractory_period_s, leak_rate_hz=0.1,
-                                     shot_noise_rate_hz=1, device=device)
+                                     shot_noise_rate_hz=1, device=device, lazy_count=lazy_count)
         self.e2v_net = CistaLSTCNet(image_dim=image_dim, base_channels=cfgs.base_channels, depth=cfgs.depth,
                                     num_bins=cfgs.num_bins)
 
