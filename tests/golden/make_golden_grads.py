@@ -14,7 +14,11 @@ g3 (grads_180x240_seq15.npz): config c3's frame size and sequence length -- 180x
     are NOT stored: tests regenerate them with oracle/fixtures.synthetic_voxels (seed below) and
     check them against the stored checksum.
 
-    PYTHONPATH=/root/reference:. python tests/golden/make_golden_grads.py [g12] [g3]
+g4 (grads_180x240_b8.npz): config c3's batch -- 180x240, B=8, 5 frames, the g2 loss -> the same
+    keys as g3 plus the fp32 reference's per-sample last frames.  The wgrad partial sums and the
+    DDP reductions depend on B; g1/g2 pin B <= 2 only.
+
+    PYTHONPATH=/root/reference:. python tests/golden/make_golden_grads.py [g12] [g3] [g4]
 """
 from __future__ import annotations
 
@@ -28,6 +32,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
 from oracle import fixtures as fx  # noqa: E402
 from tests.golden.g3_spec import G3, g3_inputs, g3_params  # noqa: E402
+from tests.golden.g4_spec import G4, g4_inputs, g4_params  # noqa: E402
 from e2v.e2v_model import CistaLSTCNet  # noqa: E402
 
 torch.set_num_threads(8)
@@ -108,10 +113,9 @@ def main():
     print("wrote", os.path.join(HERE, "grads_32x48.npz"))
 
 
-def main_g3():
-    c = G3
-    params = g3_params()
-    vox, target = g3_inputs()
+def main_g3(c=G3, params_fn=g3_params, inputs_fn=g3_inputs, name="grads_180x240_seq15.npz"):
+    params = params_fn()
+    vox, target = inputs_fn()
     res = {"vox_sum": np.float64(vox.astype(np.float64).sum()),
            "vox_abs_sum": np.float64(np.abs(vox.astype(np.float64)).sum())}
     grads = {}
@@ -130,6 +134,7 @@ def main_g3():
         res[f"{tag}_loss"] = np.float64(loss.item())
         res[f"{tag}_last_frame"] = out.detach().double().numpy().astype(np.float32)
         grads[tag] = unique_grads(m, c["depth"])
+        del m, out, state, prev, loss                       # free the autograd graph (B=8: ~13 / 27 GB)
     for k, v in grads["f32"].items():
         res[f"f32_param_{k}"] = v.astype(np.float32)
         v64 = grads["f64"][k]
@@ -137,14 +142,16 @@ def main_g3():
         res[f"noise32_param_{k}"] = np.float64(np.abs(v - v64).max() / max(np.abs(v64).max(), 1e-30))
     for k, v in c.items():
         res[f"cfg_{k}"] = np.float64(v)
-    path = os.path.join(HERE, "grads_180x240_seq15.npz")
+    path = os.path.join(HERE, name)
     np.savez_compressed(path, **res)
     print("wrote", path)
 
 
 if __name__ == "__main__":
-    which = sys.argv[1:] or ["g12", "g3"]
+    which = sys.argv[1:] or ["g12", "g3", "g4"]
     if "g12" in which:
         main()
     if "g3" in which:
         main_g3()
+    if "g4" in which:
+        main_g3(G4, g4_params, g4_inputs, "grads_180x240_b8.npz")

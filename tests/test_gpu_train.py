@@ -160,3 +160,38 @@ def test_c3_size_bptt_against_fp64_truth(golden):
     print("\n" + "\n".join(f"  c3 grad {k:40s} hip-vs-f64 {e:.2e}   ref32-vs-f64 {n:.2e}"
                             for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]))
     assert not bad, bad
+
+
+def test_c3_batch8_bptt_against_fp64_truth(golden):
+    """BASELINE config c3's batch (and c4's per-rank shape): 180x240, B=8, 5 frames of
+    train_e2v.py:108-130.  The split-wgrad partial sums are split over the B x tiles pixel tiles
+    (cista_backward.hpp wgrad_split_kernel), so their grid depends on B: g1/g2 pin B <= 2 only."""
+    from tests.golden.g4_spec import G4, g4_inputs, g4_params
+    d = golden("grads_180x240_b8.npz")
+    vox, target = g4_inputs()
+    assert float(vox.astype(np.float64).sum()) == float(d["vox_sum"])     # same inputs as the generator
+    c = G4
+    m = CistaLSTCNet([c["H"], c["W"]], base_channels=c["C"], depth=c["depth"], num_bins=5)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in g4_params().items()}, c["depth"])
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    prev = torch.zeros(c["B"], 1, c["H"], c["W"], device=DEV)
+    state = None
+    for s in range(c["L"]):
+        out, state = m(gpu(vox[s]), prev, state)
+        prev = out.clone()
+    loss = torch.nn.functional.l1_loss(out, gpu(target))
+    loss.backward()
+    torch.cuda.synchronize()
+    assert rel_err(out.detach().cpu().numpy(), d["f32_last_frame"]) < 1e-4
+    assert abs(loss.item() - float(d["f64_loss"])) <= 1e-4 * abs(float(d["f64_loss"]))
+    bad, rows = {}, []
+    for k, g in grads_by_name(m).items():
+        e = rel_err(g, d[f"f64_param_{k}"])
+        bar = max(4 * float(d[f"noise32_param_{k}"]), 5e-4)
+        rows.append((k, e, float(d[f"noise32_param_{k}"])))
+        if not e <= bar:
+            bad[k] = (e, bar)
+    print("\n" + "\n".join(f"  c3 B=8 grad {k:40s} hip-vs-f64 {e:.2e}   ref32-vs-f64 {n:.2e}"
+                            for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]))
+    assert not bad, bad

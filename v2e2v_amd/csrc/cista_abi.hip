@@ -1224,6 +1224,9 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
     hipStream_t st = static_cast<hipStream_t>(stream);
     const int C = cfg->base_channels, nb = cfg->num_bins;
     const Layout L = make_layout(*cfg);
+    // alignment gaps included: the packed bytes are a function of the parameters alone (data-
+    // parallel replicas compare them bitwise)
+    if (hipMemsetAsync(packed, 0, L.total, st) != hipSuccess) return CISTA_ERR_HIP;
     {
         const long ne = 9L * 25 * (nb + 1) * C + C;
         hipLaunchKernelGGL(compose_in_w0_kernel, dim3((unsigned)((ne + 255) / 256)), dim3(256), 0, st,

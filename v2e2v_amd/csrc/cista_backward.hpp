@@ -366,13 +366,23 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 //                               column-shifted 8 x 16 copies (dx = 0, 1, 2), so that every
 //                               tap's B fragment is one aligned ds_read_b128.
 // Row strides GST = 104 and XST = 136 halves put the 16 lanes of a fragment read on 16
-// distinct 16-byte bank groups.  X needs no scale: it is a forward conv input, already bound
-// by the forward's split to |x| < 65504.  Per-split partials as wgrad_kernel (same reduce).
+// distinct 16-byte bank groups (ds_read_b128: 16-lane groups, 64 banks).  The staging stores
+// (ds_write_b128: 8-lane groups, 32 banks) are conflict-free by the item order: G item
+// i = 12 cq + pg (pixel group pg fastest) -- 8 consecutive items write 128 contiguous bytes of
+// one co row, or the tail of one row and the head of the row 4 below it, which is 832 B = 64
+// mod 128 further on; X item = (column half xcg fastest, halo row xr, channel pair xp), so the
+// 8 lanes of a group write one plane's 128 contiguous bytes.  All 256 threads stage X (channel
+// pairs, float2 loads), 192 stage G.
+// Range: X is a forward activation with no per-tensor scale.  Every tile's X maximum is reduced
+// across the workgroup (on the barrier that is there anyway); once it reaches 16384 the
+// workgroup switches to a power-of-two pre-scale sx of X (the accumulators, in units of sx,
+// are rescaled exactly) -- gradients stay fp32-faithful for activations beyond the fp16 range.
+// Per-split partials as wgrad_kernel (same reduce).
 // --------------------------------------------------------------------------------------------
 constexpr int WS_TH = 6, WS_TW = 16, WS_NPX = 96, WS_HH = 8, WS_HW = 18;
 constexpr int WS_GST = WS_NPX + 8;                  // halves per co row
 constexpr int WS_XST = WS_HH * WS_TW + 8;           // halves per (dx, ci) plane
-constexpr size_t WS_LDS = (size_t)2 * 64 * WS_GST * 2 + (size_t)2 * 3 * 32 * WS_XST * 2;
+constexpr size_t WS_LDS = (size_t)2 * 64 * WS_GST * 2 + (size_t)2 * 3 * 32 * WS_XST * 2 + 16;   // + X maxima
 
 __device__ __forceinline__ void split_pack8(const float (&v)[8], u32x4 &hi, u32x4 &lo) {
     f16x8 h, l;
@@ -386,10 +396,22 @@ __device__ __forceinline__ void split_pack8(const float (&v)[8], u32x4 &hi, u32x
     lo = __builtin_bit_cast(u32x4, l);
 }
 
+// two consecutive input channels ci, ci + 1 of the reflect-padded NHWC input (ci even)
+__device__ __forceinline__ float2 wg_load_x2(const WgradArgs &a, int b, int iy, int ix, int ci) {
+    const bool s0 = ci < a.x0c;
+    const float *seg = s0 ? a.X0 : a.X1;
+    const int segC = s0 ? a.x0c : a.x1c;
+    const int cc = s0 ? ci : ci - a.x0c;
+    if (!seg || ci >= a.Cin) return make_float2(0.f, 0.f);
+    const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
+    return *reinterpret_cast<const float2 *>(seg + (((size_t)b * a.Hin + y) * a.Win + x) * segC + cc);
+}
+
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
     _Float16 *Gs = reinterpret_cast<_Float16 *>(wsm4);           // [2][64][GST]
     _Float16 *Xs = Gs + 2 * 64 * WS_GST;                          // [2][3][32][XST]
+    float *xmx = reinterpret_cast<float *>(Xs + 2 * 3 * 32 * WS_XST);   // [4] per-wave X maxima
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nci = a.Cin / 32;
     const int co0 = (blockIdx.x / nci) * 64, ci0 = (blockIdx.x % nci) * 32;
@@ -403,15 +425,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
     const bool do_bias = a.bpartial && (blockIdx.x % nci) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
-    // staging items: G (tid < 192): co quad cq = tid & 15, pixel group pg = tid >> 4 (8 px);
-    //                X (tid < 128): ci quad xq = tid & 7, halo row r = (tid >> 3) & 7, column
-    //                group cg = tid >> 6 (halo columns 8 cg .. 8 cg + 9)
-    const int cq = tid & 15, pg = tid >> 4;
-    const int xq = tid & 7, xr = (tid >> 3) & 7, xcg = (tid >> 6) & 1;
+    // staging items: G (tid < 192): co quad cq, pixel group pg (8 px), i = 12 cq + pg;
+    //                X (all): column half xcg = tid & 1 (halo columns 8 xcg .. 8 xcg + 9), halo
+    //                row xr = (tid >> 1) & 7, channel pair xp = tid >> 4 (ci 2 xp, 2 xp + 1)
+    const int cq = tid / 12, pg = tid - cq * 12;
+    const int xcg = tid & 1, xr = (tid >> 1) & 7, xp = tid >> 4;
     // the global loads of BOTH operands of the next pixel tile are issued right after this
     // tile's LDS image is written, so they land under its MFMAs (register double buffer);
     // the split + LDS stores of a tile wait only for loads issued a whole tile earlier
-    float4 gv[8], xv[10];
+    float4 gv[8];
+    float2 xv[10];
     auto load_tile = [&](int tile) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
@@ -430,15 +453,36 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                         a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 4 * cq);
             }
         }
-        if (tid < 128) {
 #pragma unroll
-            for (int j = 0; j < 10; ++j)
-                xv[j] = wg_load_x4<XS_S1>(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 4 * xq);
-        }
+        for (int j = 0; j < 10; ++j) xv[j] = wg_load_x2(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 2 * xp);
     };
+    float sx = 1.0f;                            // X pre-scale in force (power of two, <= 1)
     if ((int)blockIdx.y < ntiles) load_tile(blockIdx.y);
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
+        {   // this tile's X maximum, reduced on the barrier that retires the previous tile's reads
+            float m = 0.0f;
+#pragma unroll
+            for (int j = 0; j < 10; ++j) m = fmaxf(m, fmaxf(fabsf(xv[j].x), fabsf(xv[j].y)));
+            for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+            if (lane == 0) xmx[wave] = m;
+        }
         __syncthreads();                       // the previous tile's fragment reads are done
+        {
+            const float m = fmaxf(fmaxf(xmx[0], xmx[1]), fmaxf(xmx[2], xmx[3]));
+            if (__builtin_expect(m >= 16384.0f && m < 3.0e38f, 0)) {
+                int e = (int)floorf(log2f(16384.0f / m));
+                e = e < -126 ? -126 : e;
+                const float st = ldexpf(1.0f, e);
+                if (st < sx) {                 // rescale what is accumulated (exact)
+                    const float r = st / sx;
+#pragma unroll
+                    for (int u = 0; u < 2; ++u)
+#pragma unroll
+                        for (int t = 0; t < 9; ++t) acc[u][t] *= r;
+                    sx = st;
+                }
+            }
+        }
         if (tid < 192) {
             if (do_bias) {
 #pragma unroll
@@ -458,30 +502,28 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                 *reinterpret_cast<u32x4 *>(Gs + (64 + row) * WS_GST + pg * 8) = lo;
             }
         }
-        if (tid < 128) {
 #pragma unroll
-            for (int c = 0; c < 4; ++c) {
-                float hs[10], ls[10];
+        for (int c = 0; c < 2; ++c) {
+            float hs[10], ls[10];
 #pragma unroll
-                for (int j = 0; j < 10; ++j) {
-                    const float x = (&xv[j].x)[c];
-                    const _Float16 hb = (_Float16)x;
-                    hs[j] = (float)hb;
-                    ls[j] = x - hs[j];
+            for (int j = 0; j < 10; ++j) {
+                const float x = (c ? xv[j].y : xv[j].x) * sx;             // exact: power of two
+                const _Float16 hb = (_Float16)x;
+                hs[j] = (float)hb;
+                ls[j] = x - hs[j];
+            }
+#pragma unroll
+            for (int dx = 0; dx < 3; ++dx) {
+                f16x8 h, l;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    h[j] = (_Float16)hs[j + dx];
+                    l[j] = (_Float16)ls[j + dx];
                 }
-#pragma unroll
-                for (int dx = 0; dx < 3; ++dx) {
-                    f16x8 h, l;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) {
-                        h[j] = (_Float16)hs[j + dx];
-                        l[j] = (_Float16)ls[j + dx];
-                    }
-                    const int plane = dx * 32 + 4 * xq + c;
-                    _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * xcg;
-                    *reinterpret_cast<u32x4 *>(d) = __builtin_bit_cast(u32x4, h);
-                    *reinterpret_cast<u32x4 *>(d + 3 * 32 * WS_XST) = __builtin_bit_cast(u32x4, l);
-                }
+                const int plane = dx * 32 + 2 * xp + c;
+                _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * xcg;
+                *reinterpret_cast<u32x4 *>(d) = __builtin_bit_cast(u32x4, h);
+                *reinterpret_cast<u32x4 *>(d + 3 * 32 * WS_XST) = __builtin_bit_cast(u32x4, l);
             }
         }
         __syncthreads();
@@ -521,14 +563,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
         float4 *red = reinterpret_cast<float4 *>(wsm4);
         if (tid < 192) red[tid] = bsum;
         __syncthreads();
-        if (tid < 64) {
+        if (tid < 64) {                        // co = tid: quad cq = tid / 4, its 12 pixel groups
             float t = 0.0f;
-            for (int k = 0; k < 12; ++k) t += (&red[k * 16 + (tid >> 2)].x)[tid & 3];
+            for (int k = 0; k < 12; ++k) t += (&red[(tid >> 2) * 12 + k].x)[tid & 3];
             a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + tid] = t;
         }
     }
     // acc[u][t][j]: row (cout) wco + 16u + 4*(lane>>4) + j, col (cin) wci + (lane & 15)
-    const float inv = a.gscale[1];
+    const float inv = a.gscale[1] * (1.0f / sx);
     float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
 #pragma unroll
     for (int u = 0; u < 2; ++u)
