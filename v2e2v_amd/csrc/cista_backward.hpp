@@ -370,9 +370,10 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 // (ds_write_b128: 8-lane groups, 32 banks) are conflict-free by the item order: G item
 // i = 12 cq + pg (pixel group pg fastest) -- 8 consecutive items write 128 contiguous bytes of
 // one co row, or the tail of one row and the head of the row 4 below it, which is 832 B = 64
-// mod 128 further on; X item = (column half xcg fastest, halo row xr, channel pair xp), so the
-// 8 lanes of a group write one plane's 128 contiguous bytes.  All 256 threads stage X (channel
-// pairs, float2 loads), 192 stage G.
+// mod 128 further on; X item = (column half xcg fastest, halo row xr, channel quad xq), so the
+// 8 lanes of a group write one plane's 128 contiguous bytes.  G is staged by threads 0..191, X
+// by threads 128..255 (float4 loads).  (Channel-pair X items on all 256 threads, float2 loads,
+// were tried: twice the load instructions and their address math cost more than the balance.)
 // Range: X is a forward activation with no per-tensor scale.  Every tile's X maximum is reduced
 // across the workgroup (on the barrier that is there anyway); once it reaches 16384 the
 // workgroup switches to a power-of-two pre-scale sx of X (the accumulators, in units of sx,
@@ -396,17 +397,6 @@ __device__ __forceinline__ void split_pack8(const float (&v)[8], u32x4 &hi, u32x
     lo = __builtin_bit_cast(u32x4, l);
 }
 
-// two consecutive input channels ci, ci + 1 of the reflect-padded NHWC input (ci even)
-__device__ __forceinline__ float2 wg_load_x2(const WgradArgs &a, int b, int iy, int ix, int ci) {
-    const bool s0 = ci < a.x0c;
-    const float *seg = s0 ? a.X0 : a.X1;
-    const int segC = s0 ? a.x0c : a.x1c;
-    const int cc = s0 ? ci : ci - a.x0c;
-    if (!seg || ci >= a.Cin) return make_float2(0.f, 0.f);
-    const int y = reflect_clamp(iy, a.Hin), x = reflect_clamp(ix, a.Win);
-    return *reinterpret_cast<const float2 *>(seg + (((size_t)b * a.Hin + y) * a.Win + x) * segC + cc);
-}
-
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
     _Float16 *Gs = reinterpret_cast<_Float16 *>(wsm4);           // [2][64][GST]
@@ -426,15 +416,15 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
     // staging items: G (tid < 192): co quad cq, pixel group pg (8 px), i = 12 cq + pg;
-    //                X (all): column half xcg = tid & 1 (halo columns 8 xcg .. 8 xcg + 9), halo
-    //                row xr = (tid >> 1) & 7, channel pair xp = tid >> 4 (ci 2 xp, 2 xp + 1)
+    //                X (tid >= 128): x = tid - 128, column half xcg = x & 1 (halo columns
+    //                8 xcg .. 8 xcg + 9), halo row xr = (x >> 1) & 7, channel quad xq = x >> 4
     const int cq = tid / 12, pg = tid - cq * 12;
-    const int xcg = tid & 1, xr = (tid >> 1) & 7, xp = tid >> 4;
+    const bool xt = tid >= 128;
+    const int xi = tid & 127, xcg = xi & 1, xr = (xi >> 1) & 7, xq = xi >> 4;
     // the global loads of BOTH operands of the next pixel tile are issued right after this
     // tile's LDS image is written, so they land under its MFMAs (register double buffer);
     // the split + LDS stores of a tile wait only for loads issued a whole tile earlier
-    float4 gv[8];
-    float2 xv[10];
+    float4 gv[8], xv[10];
     auto load_tile = [&](int tile) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
@@ -453,16 +443,21 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                         a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 4 * cq);
             }
         }
+        if (xt) {
 #pragma unroll
-        for (int j = 0; j < 10; ++j) xv[j] = wg_load_x2(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 2 * xp);
+            for (int j = 0; j < 10; ++j)
+                xv[j] = wg_load_x4<XS_S1>(a, b, oy0 - 1 + xr, ox0 - 1 + 8 * xcg + j, ci0 + 4 * xq);
+        }
     };
     float sx = 1.0f;                            // X pre-scale in force (power of two, <= 1)
     if ((int)blockIdx.y < ntiles) load_tile(blockIdx.y);
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit) {
         {   // this tile's X maximum, reduced on the barrier that retires the previous tile's reads
             float m = 0.0f;
+            if (xt)
 #pragma unroll
-            for (int j = 0; j < 10; ++j) m = fmaxf(m, fmaxf(fabsf(xv[j].x), fabsf(xv[j].y)));
+                for (int j = 0; j < 10; ++j)
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[j].x), fabsf(xv[j].y)), fmaxf(fabsf(xv[j].z), fabsf(xv[j].w))));
             for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
             if (lane == 0) xmx[wave] = m;
         }
@@ -502,12 +497,14 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                 *reinterpret_cast<u32x4 *>(Gs + (64 + row) * WS_GST + pg * 8) = lo;
             }
         }
+        if (xt)
 #pragma unroll
-        for (int c = 0; c < 2; ++c) {
+        for (int c = 0; c < 4; ++c) {
             float hs[10], ls[10];
 #pragma unroll
             for (int j = 0; j < 10; ++j) {
-                const float x = (c ? xv[j].y : xv[j].x) * sx;             // exact: power of two
+                float x = (&xv[j].x)[c];
+                if (__builtin_expect(sx != 1.0f, 0)) x *= sx;             // exact: power of two
                 const _Float16 hb = (_Float16)x;
                 hs[j] = (float)hb;
                 ls[j] = x - hs[j];
@@ -520,7 +517,7 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                     h[j] = (_Float16)hs[j + dx];
                     l[j] = (_Float16)ls[j + dx];
                 }
-                const int plane = dx * 32 + 2 * xp + c;
+                const int plane = dx * 32 + 4 * xq + c;
                 _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * xcg;
                 *reinterpret_cast<u32x4 *>(d) = __builtin_bit_cast(u32x4, h);
                 *reinterpret_cast<u32x4 *>(d + 3 * 32 * WS_XST) = __builtin_bit_cast(u32x4, l);
