@@ -25,6 +25,7 @@ from __future__ import annotations
 import argparse
 import ctypes
 import json
+import re
 import math
 import os
 import sys
@@ -143,6 +144,28 @@ def v2e2v_main(args, torch, vd, rank, world, device):
         vd.barrier()
         elapsed = vd.max_over_ranks(time.perf_counter() - t0, device)
     frames_done = world * B * L * args.steps
+    from v2e2v_amd import _lib
+    # the dominant kernel of the reconstruction at this size (HIP events on the library's stream)
+    vlast = net.event_voxel_grids
+    layers = time_layers(torch, net.e2v_net, _lib, torch.stack([vlast, vlast]), B, H, W, device, args.layer_reps)
+    roofline = dominant_roofline(layers, _lib, traffic_tag="v2e2v")
+    # the emulator alone: one pack of P frames (diff / iters / emit per frame + preprocess)
+    with torch.no_grad():
+        frames = vid[:P].permute(1, 0, 2, 3).contiguous()
+        net.v2e_net.reset()
+        ts0 = (dt * torch.arange(P, dtype=torch.float64)).repeat(B, 1)
+        net.v2e_net(frames, ts0)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        reps = 10
+        e0.record()
+        for r in range(reps):
+            net.v2e_net(frames, ts0 + (r + 1) * P * dt)
+        e1.record()
+        e1.synchronize()
+        v2e_ms = e0.elapsed_time(e1) / reps
+    cpu = None
+    if rank == 0 and not args.no_cpu_baseline:
+        cpu = v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt)
     if rank == 0:
         print(json.dumps({
             "metric": "V2E2V reconstructed frames/sec (v2e emulator + CISTA-LSTC) at 720x1280",
@@ -154,10 +177,67 @@ def v2e2v_main(args, torch, vd, rank, world, device):
             "config": {"workload": f"V2E2V {H}x{W}, num_pack_frames={P}, len_sequence={L}, {B} video/GPU",
                        "batch_per_gpu": B, "len_sequence": L, "num_pack_frames": P,
                        "parallelism": f"replicas x{world}"},
-            "events_last_pack": int(net.num_events), "outputs_finite": bool(torch.isfinite(rec).all())}),
+            "events_last_pack": int(net.num_events), "outputs_finite": bool(torch.isfinite(rec).all()),
+            "roofline": roofline, "cpu_baseline": cpu,
+            "emulator_ms_per_pack": round(v2e_ms, 4),
+            "reconstruction_ms_per_frame_kernels": round(sum(v["ms"] * v["launches_per_frame"]
+                                                             for v in layers.values()), 4),
+            "layers_ms": {k: round(v["ms"], 4) for k, v in layers.items()}}),
             flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+class _NpRng:
+    """The random source the emulator restatement draws from (numpy; the GPU emulator's Philox
+    stream is not reproduced -- the CPU leg is a timing sample, not a parity check)."""
+
+    def __init__(self, seed):
+        import numpy as np
+        self.g = np.random.default_rng(seed)
+
+    def normal(self, mean, std, shape):
+        return self.g.normal(mean, std, shape)
+
+    def randn(self, shape):
+        return self.g.standard_normal(shape, dtype="float32")
+
+    def rand(self, shape):
+        return self.g.random(shape, dtype="float32")
+
+
+def v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt, min_s=10.0, max_recs=6):
+    """cpu_baseline leg of config c5: the emulator restated in numpy (oracle/v2e_oracle.py:
+    EventEmulator voxel-grid mode, the V2E2VNet noise settings) + event_preprocess + the
+    CISTA-LSTC forward on ATen's CPU kernels (oracle/cista_oracle_torch.py), B=1, reconstruction
+    after reconstruction (states and previous image carried) until >= min_s seconds."""
+    import numpy as np
+    from oracle import fixtures as fx
+    from oracle import v2e_oracle as vo
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU
+    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    torch.set_num_threads(cores)
+    e2v = net.e2v_net
+    sd = {k: v.detach().cpu().numpy() for k, v in e2v.state_dict().items()}
+    ref = CistaLSTCTorchCPU(fx.collapse_tied(sd, e2v.depth), e2v.depth)
+    emu = vo.V2EOracle(num_bins=cfgs.num_bins, pos_thres=cfgs.C, neg_thres=cfgs.C, sigma_thres=cfgs.threshold_sigma,
+                       cutoff_hz=cfgs.cutoff_hz, refractory_period_s=cfgs.refractory_period_s, leak_rate_hz=0.1,
+                       shot_noise_rate_hz=1.0, rng=_NpRng(0))
+    n_avail = (vid.shape[0] - 1) // (P - 1)
+    prev, states, recs, t = torch.zeros(1, 1, H, W), None, 0, 0.0
+    while recs < min(max_recs, n_avail) and (t < min_s or recs == 0):
+        fr = vid[recs * (P - 1): recs * (P - 1) + P, :1].permute(1, 0, 2, 3).cpu().numpy()
+        ts = (recs * (P - 1) + np.arange(P)[None]) * dt
+        t0 = time.perf_counter()
+        vox, _ = emu.forward(fr, ts)
+        v = torch.from_numpy(np.ascontiguousarray(vo.preprocess_whole(vox)))
+        prev, states = ref.forward(v, prev, states)
+        t += time.perf_counter() - t0
+        recs += 1
+    return dict(value=recs / t, unit="frames/s", cores=int(cores), kind="port",
+                sample=f"{recs} reconstruction(s) at {H}x{W} (B=1), each a {P}-frame pack through the numpy "
+                       f"emulator restatement (oracle/v2e_oracle.py) + the PyTorch-CPU CISTA-LSTC restatement "
+                       f"(oracle/cista_oracle_torch.py), {cores} threads, {t:.1f} s")
 
 
 def train_main(args, torch, vd, rank, world, device):
@@ -398,6 +478,52 @@ def time_layers(torch, model, lib_mod, vox, B, H, W, device, reps):
     return res
 
 
+def dominant_roofline(layers, lib_mod, traffic_tag=None):
+    """The roofline object of the frame's dominant kernel (largest ms x launches per frame):
+    algorithmic FLOPs of one launch / its mean duration (HIP events, time_layers), against the
+    split3 peak; HBM bytes per launch from the committed PMC passes (profiles/*pmc_traffic.json)
+    when they were measured on this build and on this workload (traffic_tag: the passes' "config"
+    field; None = the headline configuration)."""
+    dom_name = max(layers, key=lambda k: layers[k]["ms"] * layers[k]["launches_per_frame"])
+    dom = layers[dom_name]
+    peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
+    roofline = dict(bound="mfma", achieved=round(dom["tflops"], 2), peak=round(peak, 1),
+                    unit="TFLOP/s", frac=round(dom["tflops"] / peak, 4), traffic=None,
+                    kernel=dom_name, launch_ms=round(dom["ms"], 4),
+                    flop_per_launch=2 * dom["macs"],
+                    note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean "
+                         "duration; peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+
+    # HBM bytes per launch of the same kernel from the committed PMC passes (FETCH_SIZE and
+    # WRITE_SIZE, separate rocprofv3 runs, gfx950 read correction): scripts/pmc_traffic.py
+    import glob
+    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
+    tag = "" if traffic_tag is None else traffic_tag + "_"
+    tfiles = [f for f in tfiles if re.fullmatch(r"r\d\d_" + tag + "pmc_traffic\.json", os.path.basename(f))]
+    if tfiles:
+        try:
+            import hashlib
+            tj = json.load(open(tfiles[-1]))
+            tl = tj["layers"].get(dom_name)
+            sha = hashlib.sha256(open(lib_mod.LIB_PATH, "rb").read()).hexdigest()
+            roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
+            if tl and tj.get("lib_sha256") == sha:
+                roofline["traffic"] = tl["hbm_bytes_per_launch"]
+                # the same launch against the HBM roof: the ISTA / Dg convs move as many bytes
+                # per FLOP as the two roofs balance, so their time is bounded by the sum of the
+                # two fractions when staging / epilogue and MFMAs do not overlap (DESIGN.md 4.7)
+                gbps = tl["hbm_bytes_per_launch"] / (dom["ms"] * 1e-3) / 1e9
+                roofline["hbm_achieved_GBps"] = round(gbps, 1)
+                roofline["hbm_frac"] = round(gbps / (HBM_TBPS * 1e3), 4)
+            else:       # measured on another build (or not this kernel): never quote stale bytes
+                roofline["traffic_note"] = ("no PMC traffic of this build's " + dom_name + " kernel in "
+                                            + roofline["traffic_source"])
+        except (OSError, ValueError, KeyError):
+            pass
+
+    return roofline
+
+
 def psnr(a, b):
     """utils/evaluate.py:18-28 (PIXEL_MAX = 1, 100 if mse < 1e-10)."""
     import numpy as np
@@ -547,40 +673,7 @@ def main():
     value = frames / elapsed
 
     layers = time_layers(torch, model, _lib, vox, B, H, W, device, args.layer_reps)
-    dom_name = max(layers, key=lambda k: layers[k]["ms"] * layers[k]["launches_per_frame"])
-    dom = layers[dom_name]
-    peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
-    roofline = dict(bound="mfma", achieved=round(dom["tflops"], 2), peak=round(peak, 1),
-                    unit="TFLOP/s", frac=round(dom["tflops"] / peak, 4), traffic=None,
-                    kernel=dom_name, launch_ms=round(dom["ms"], 4),
-                    flop_per_launch=2 * dom["macs"],
-                    note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean "
-                         "duration; peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
-
-    # HBM bytes per launch of the same kernel from the committed PMC passes (FETCH_SIZE and
-    # WRITE_SIZE, separate rocprofv3 runs, gfx950 read correction): scripts/pmc_traffic.py
-    import glob
-    tfiles = sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc_traffic.json")))
-    if tfiles:
-        try:
-            import hashlib
-            tj = json.load(open(tfiles[-1]))
-            tl = tj["layers"].get(dom_name)
-            sha = hashlib.sha256(open(_lib.LIB_PATH, "rb").read()).hexdigest()
-            roofline["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
-            if tl and tj.get("lib_sha256") == sha:
-                roofline["traffic"] = tl["hbm_bytes_per_launch"]
-                # the same launch against the HBM roof: the ISTA / Dg convs move as many bytes
-                # per FLOP as the two roofs balance, so their time is bounded by the sum of the
-                # two fractions when staging / epilogue and MFMAs do not overlap
-                gbps = tl["hbm_bytes_per_launch"] / (dom["ms"] * 1e-3) / 1e9
-                roofline["hbm_achieved_GBps"] = round(gbps, 1)
-                roofline["hbm_frac"] = round(gbps / (HBM_TBPS * 1e3), 4)
-            else:       # measured on another build (or not this kernel): never quote stale bytes
-                roofline["traffic_note"] = ("no PMC traffic of this build's " + dom_name + " kernel in "
-                                            + roofline["traffic_source"])
-        except (OSError, ValueError, KeyError):
-            pass
+    roofline = dominant_roofline(layers, _lib)
 
     voxelizer = (time_voxelizer(torch, B * L, args.num_events, nb, H, W, device, cpu_leg=not args.no_cpu_baseline)
                  if rank == 0 else None)

@@ -365,8 +365,8 @@ __global__ __launch_bounds__(256) void wgrad_kernel(const WgradArgs a) {
 //   Xs[part][dx][ci][XST]       the reflect-padded input halo (8 rows x 18 cols) as three
 //                               column-shifted 8 x 16 copies (dx = 0, 1, 2), so that every
 //                               tap's B fragment is one aligned ds_read_b128.
-// Row strides GST = 104 and XST = 136 halves put the 16 lanes of a fragment read on 16
-// distinct 16-byte bank groups (ds_read_b128: 16-lane groups, 64 banks).  The staging stores
+// Row strides GST = 104 and XST = 136 halves (odd in 16-byte units) with the pair swizzle of
+// ws_swz put the 16 lanes of each ds_read_b128 lane group on 16 distinct 16-byte bank groups.  The staging stores
 // (ds_write_b128: 8-lane groups, 32 banks) are conflict-free by the item order: G item
 // i = 12 cq + pg (pixel group pg fastest) -- 8 consecutive items write 128 contiguous bytes of
 // one co row, or the tail of one row and the head of the row 4 below it, which is 832 B = 64
@@ -396,6 +396,12 @@ __device__ __forceinline__ void split_pack8(const float (&v)[8], u32x4 &hi, u32x
     hi = __builtin_bit_cast(u32x4, h);
     lo = __builtin_bit_cast(u32x4, l);
 }
+
+// fragment-read swizzle: rows (co) / planes (ci) r with bit 2 != bit 3 keep their 8-pixel groups
+// pairwise swapped (group j stored in slot j ^ 1), so the lane groups of ds_read_b128 ({0-3,12-15,
+// 20-27}, ...: rows r = 0-3,12-15 at K slot kg beside rows 4-11 at kg + 1) hit 16 distinct bank
+// groups for any odd row stride (16-byte units) -- without it every read was 2-way (8 cycles, not 4)
+__device__ __forceinline__ int ws_swz(int r) { return ((r >> 2) ^ (r >> 3)) & 1; }
 
 __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
@@ -492,9 +498,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                 for (int j = 0; j < 8; ++j) v[j] = (&gv[j].x)[c] * gsc;    // exact: power of two
                 u32x4 hi, lo;
                 split_pack8(v, hi, lo);
-                const int row = 4 * cq + c;
-                *reinterpret_cast<u32x4 *>(Gs + row * WS_GST + pg * 8) = hi;
-                *reinterpret_cast<u32x4 *>(Gs + (64 + row) * WS_GST + pg * 8) = lo;
+                const int row = 4 * cq + c, slot = (pg ^ ws_swz(row)) * 8;
+                *reinterpret_cast<u32x4 *>(Gs + row * WS_GST + slot) = hi;
+                *reinterpret_cast<u32x4 *>(Gs + (64 + row) * WS_GST + slot) = lo;
             }
         }
         if (xt)
@@ -518,18 +524,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
                     l[j] = (_Float16)ls[j + dx];
                 }
                 const int plane = dx * 32 + 4 * xq + c;
-                _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * xcg;
+                _Float16 *d = Xs + plane * WS_XST + xr * WS_TW + 8 * (xcg ^ ws_swz(4 * xq + c));
                 *reinterpret_cast<u32x4 *>(d) = __builtin_bit_cast(u32x4, h);
                 *reinterpret_cast<u32x4 *>(d + 3 * 32 * WS_XST) = __builtin_bit_cast(u32x4, l);
             }
         }
         __syncthreads();
         if (tile + a.nsplit < ntiles) load_tile(tile + a.nsplit);
-        const int kg = lane >> 4, r16 = lane & 15;
+        const int kg = lane >> 4, r16 = lane & 15, ks = kg ^ ws_swz(r16);
 #pragma unroll
         for (int s = 0; s < WS_NPX / 32; ++s) {
-            const int p0 = 32 * s + 8 * kg;
-            const int py = p0 >> 4, px0 = p0 & 15;
+            const int p0 = 32 * s + 8 * ks;                         // stored slot of pixel group 4 s + kg
+            const int py = 2 * s + (kg >> 1), px0 = 8 * (ks & 1);
             u32x4 ah[2], al[2];
 #pragma unroll
             for (int u = 0; u < 2; ++u) {

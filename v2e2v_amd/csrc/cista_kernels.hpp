@@ -58,6 +58,14 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_RANGE_CHECK
 #define CISTA_RANGE_CHECK 1
 #endif
+// timing experiment: the workgroups of the first dispatch round (blockIdx < 512) sleep a
+// pseudo-random 0 .. CISTA_EXP_JITTER shader cycles before starting (breaks chip-wide lock-step)
+#ifndef CISTA_EXP_JITTER
+#define CISTA_EXP_JITTER 0
+#endif
+#ifndef CISTA_AORDER
+#define CISTA_AORDER 0
+#endif
 #ifndef CISTA_RERUN
 #define CISTA_RERUN 1
 #endif
@@ -499,6 +507,12 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wl, acc[m][n], 0, 0, 0);
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wh, acc[m][n], 0, 0, 0);
         }
+#if CISTA_AORDER
+        // the next m-tile's two A reads go out BEFORE this m-tile's MFMAs (left to itself the
+        // scheduler sinks them below 2/3 of the MFMAs, ~32 cycles before their use)
+        if (m + 1 < MT_W) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x8, 3 * NW, 0);
+#endif
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -649,6 +663,13 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         CISTA_STAMP(0, (unsigned long long)hw | ((unsigned long long)xcc << 32));
         CISTA_STAMP(13, __builtin_amdgcn_s_memrealtime());
         CISTA_STAMP(1, __builtin_amdgcn_s_memtime());
+    }
+#endif
+#if CISTA_EXP_JITTER
+    if (blockIdx.x < 512u) {
+        const unsigned hsh = (blockIdx.x * 2654435761u) >> 16;
+        const unsigned long long until = __builtin_amdgcn_s_memtime() + (unsigned long long)(hsh % 1024u) * CISTA_EXP_JITTER / 1024u;
+        while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(4);
     }
 #endif
     const int wm = wave % WM;
