@@ -9,6 +9,8 @@ event count exactly, the normalised voxels to TOL of their max (both use event_p
 float32 statistics; the sums are rounded once, so the mean / std may differ in the last bit).
 The random configuration is checked for reproducibility per seed and for plausible statistics.
 """
+import math
+
 import numpy as np
 import pytest
 import torch
@@ -90,6 +92,30 @@ def test_random_configuration_reproducible_and_plausible():
     # normalised like event_preprocess_pytorch: mean 0 / std 1 over the non-zero voxels
     nz = vox[vox != 0]
     assert abs(float(nz.mean())) < 1e-3 and abs(float(nz.std()) - 1.0) < 1e-2
+
+
+def test_shot_noise_rate_matches_its_expectation():
+    """generate_shot_noise (emulator_utils.py:159-207): a pixel whose polarity is set but whose
+    count is below the iteration index fires with probability factor * pos_pre per iteration
+    (r > 1 - factor * pos_pre).  One frame step, no threshold spread / leak / refractory: a
+    bright block sets max_num_iters = 4, the background (+0.5 grey levels: polarity +1, count 0)
+    fires by shot noise only; the event total must sit within 5 sigma of its expectation."""
+    H, W, shot, dt = 64, 80, 100.0, 0.01
+    fr = np.full((1, 2, H, W), 100.0, np.float32)
+    fr[0, 1] = 100.5
+    fr[0, 1, 8:16, 8:24] = 255.0
+    tf = times(1, 2, 0.0, dt=dt)
+    e = v2e.EventEmulator("voxel_grid", device="cuda", seed=9, sigma_thres=0.0, leak_rate_hz=0.0,
+                          shot_noise_rate_hz=shot, cutoff_hz=0.0, refractory_period_s=0.0)
+    _, n = e(torch.from_numpy(fr).cuda(), torch.from_numpy(tf))
+    cnt = int(np.floor(abs(np.log(255.0) - np.log(100.0)) / 0.2))         # the block's count
+    assert cnt == 4
+    inten = (np.float32(100.5) + 20) / 275
+    p = shot / 2 * dt / cnt * ((0.25 - 1) * inten + 1)                    # per iteration
+    n_bg = H * W - 8 * 16
+    mean = 8 * 16 * cnt + n_bg * cnt * p
+    sd = math.sqrt(n_bg * cnt * p * (1 - p))
+    assert abs(int(n) - mean) < 5 * sd, (int(n), mean, sd)
 
 
 def test_time_must_increase():

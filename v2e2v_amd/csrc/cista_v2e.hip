@@ -56,9 +56,6 @@ __device__ __forceinline__ float randn(unsigned long long seed, unsigned long lo
     const U4 r = draw(seed, d, e);
     return sqrtf(-2.0f * logf(u01(r.x))) * cosf(6.28318530717958647692f * u01(r.y));
 }
-__device__ __forceinline__ float rand01(unsigned long long seed, unsigned long long d, unsigned long long e) {
-    return u01(draw(seed, d, e).x);
-}
 
 // ------------------------------------------------------------------ per-call constants
 struct Call {
@@ -79,18 +76,27 @@ struct State {   // device planes, B*H*W each
 };
 
 constexpr int MAXSLOTS = 64;    // atomic slots per batch element of the image max
+constexpr int SLOTW = 32;       // 4-byte words per slot: one 128-byte line each (same-line atomics
+                                // serialise in L2: 3600 workgroups on 2 lines took ~20 us)
 
 struct Scratch {
     int *counts;          // B*H*W event counts of the current frame
     float *pol;           // B*H*W polarity (+1 / -1 / 0)
-    int *iters_raw;       // [B][MAXSLOTS] image max of counts (partial maxima)
+    int *iters_raw;       // [B][MAXSLOTS][SLOTW] image max of counts (partial maxima, word 0 of a slot)
     int *num_iters;       // [B] max(iters_raw, 1)
     float *ts_step;       // [B]
     int *meta;            // [0] max_num_iters, [1] refractory switch
-    unsigned long long *nev;
+    unsigned long long *nev;   // [MAXSLOTS][SLOTW / 2] partial event totals (workgroup mod MAXSLOTS)
 };
 
+#ifndef CISTA_V2E_EXP
+#define CISTA_V2E_EXP 0   // timing-only switch (results WRONG when set): 1 float log, 2 no leak draw
+#endif
+
 __device__ __forceinline__ float lin_log(float v, double f) {
+#if CISTA_V2E_EXP == 1
+    return v <= 20.0f ? v * (float)f : logf(v);
+#endif
     // emulator_utils.py:13-38 (float64, rounded to 8 decimals, half to even like torch.round)
     const double x = (double)v;
     double y = x <= 20.0 ? x * f : log(x);
@@ -138,38 +144,48 @@ __global__ void v2e_tmem_kernel(Call c, State s) {
 
 __global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch w, const float *frames, int n,
                                                        float dt_frame) {
-    const long long HW = (long long)c.H * c.W;
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int HW = c.H * c.W;                  // B * H * W < 2^31 (checked on the host)
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const cista_v2e_config &g = c.cfg;
     int cnt = 0;
     int b = 0;
-    if (i < (long long)c.B * HW) {
-        b = (int)(i / HW);
-        const long long p = i - b * HW;
-        const int y = (int)(p / c.W), x = (int)(p - (long long)y * c.W);
-        const float fr = frames[((long long)b * c.F + n) * HW + p];
+    if (i < c.B * HW) {
+        b = i / HW;
+        const int p = i - b * HW;
+        const int y = p / c.W, x = p - y * c.W;
+        // every load is issued before the first store and before the long lin_log: the waves
+        // wait for memory once (issued in program order after stores they were 5 round trips)
+        const bool lowpass = g.cutoff_hz > 0.0f, leak = g.leak_rate_hz > 0.0f;
+        const float fr = frames[((size_t)b * c.F + n) * HW + p];
+        const float lp_old = lowpass ? s.lp[i] : 0.0f;
+        float base = s.base[i];
+        const float nrate = leak ? s.noise_rate[i] : 0.0f;
+        const float pos = s.pos[i], neg = s.neg[i];
         float nw = lin_log(fr, c.linlog_f);
-        if (g.cutoff_hz > 0.0f) {                              // low_pass_filter (:49-101)
+        if (lowpass) {                                         // low_pass_filter (:49-101)
             const float inten = rescale(fr);
             const bool half = (y % 2 == 0) && (x % 2 == 0);
             float eps = g.ql > 0.0f ? inten * c.dt_lp0[n] : 1.0f;
             if (half) eps = g.qs > 0.0f ? inten * c.dt_lp1[n] : 1.0f;
             eps = fminf(eps, 1.0f);
-            nw = (1.0f - eps) * s.lp[i] + eps * nw;
-            s.lp[i] = nw;
+            nw = (1.0f - eps) * lp_old + eps * nw;
         }
-        float base = s.base[i];
-        if (g.leak_rate_hz > 0.0f) {                           // subtract_leak_current (:104-124)
+        if (leak) {                                            // subtract_leak_current (:104-124)
+#if CISTA_V2E_EXP == 2
+            const float r = 0.0f;
+#else
             const float r = randn(c.seed, c.draw0 + 8 + 2 * (unsigned long long)n, i);
-            const float rate = g.leak_rate_hz * s.noise_rate[i] * (1.0f - g.leak_jitter_fraction * r);
-            base = base - dt_frame * rate * s.pos[i];
-            s.base[i] = base;
+#endif
+            const float rate = g.leak_rate_hz * nrate * (1.0f - g.leak_jitter_fraction * r);
+            base = base - dt_frame * rate * pos;
         }
         float diff = nw - base;                                // :386
         if (!(fabsf(diff) > 1e-6f)) diff = 0.0f;               // :405-406
         const float pol = diff > 0.0f ? 1.0f : (diff < 0.0f ? -1.0f : 0.0f);
-        const float C = (pol > 0.0f ? s.pos[i] : 0.0f) + (pol < 0.0f ? s.neg[i] : 0.0f);   // :412
+        const float C = (pol > 0.0f ? pos : 0.0f) + (pol < 0.0f ? neg : 0.0f);   // :412
         cnt = (int)floorf(fabsf(diff) / (C + 1e-9f));          // :413
+        if (lowpass) s.lp[i] = nw;
+        if (leak) s.base[i] = base;
         w.counts[i] = cnt;
         w.pol[i] = pol;
     }
@@ -181,11 +197,12 @@ __global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch 
     for (int o = 32; o > 0; o >>= 1) m = max(m, __shfl_xor(m, o));
     const int b0 = __shfl(b, 0);
     const bool uniform = __all(b == b0);
-    const bool live = i - (threadIdx.x & 63) < (long long)c.B * HW;      // the wave has pixels
+    const bool live = i - (int)(threadIdx.x & 63) < c.B * HW;            // the wave has pixels
     if (uniform) {
         if ((threadIdx.x & 63) == 0) { wmax[threadIdx.x >> 6] = live ? m : 0; wb[threadIdx.x >> 6] = live ? b0 : -1; }
     } else {
-        if (i < (long long)c.B * HW) atomicMax(w.iters_raw + (size_t)b * MAXSLOTS + blockIdx.x % MAXSLOTS, cnt);
+        if (i < c.B * HW && cnt > 0)       // the slots start at 0: a zero maximum changes nothing
+            atomicMax(w.iters_raw + ((size_t)b * MAXSLOTS + blockIdx.x % MAXSLOTS) * SLOTW, cnt);
         if ((threadIdx.x & 63) == 0) { wmax[threadIdx.x >> 6] = 0; wb[threadIdx.x >> 6] = -1; }
     }
     __syncthreads();
@@ -196,7 +213,7 @@ __global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch 
             int mk = wmax[k];
             for (int l = k + 1; l < 4; ++l)
                 if (wb[l] == wb[k]) { mk = max(mk, wmax[l]); wb[l] = -1; }
-            atomicMax(w.iters_raw + (size_t)wb[k] * MAXSLOTS + blockIdx.x % MAXSLOTS, mk);
+            if (mk > 0) atomicMax(w.iters_raw + ((size_t)wb[k] * MAXSLOTS + blockIdx.x % MAXSLOTS) * SLOTW, mk);
         }
     }
 }
@@ -206,7 +223,10 @@ __global__ void v2e_iters_kernel(Call c, Scratch w) {
     int mx = 0;
     for (int b = 0; b < c.B; ++b) {
         int r = 0;
-        for (int k = 0; k < MAXSLOTS; ++k) r = max(r, w.iters_raw[(size_t)b * MAXSLOTS + k]);
+        for (int k = 0; k < MAXSLOTS; ++k) {          // read, then cleared for the next frame's diff
+            r = max(r, w.iters_raw[((size_t)b * MAXSLOTS + k) * SLOTW]);
+            w.iters_raw[((size_t)b * MAXSLOTS + k) * SLOTW] = 0;
+        }
         mx = max(mx, r);                                       // max_num_iters (:417)
         const int ni = r == 0 ? 1 : r;                         // :426
         w.num_iters[b] = ni;
@@ -219,72 +239,121 @@ __global__ void v2e_iters_kernel(Call c, Scratch w) {
     w.meta[1] = refr;
 }
 
+// The voxel cells of a pixel are touched by this thread only, so they are loaded once (at the
+// pixel's first event) and accumulated in registers, in the reference's order -- bit-identical
+// to a read-modify-write per event (a cell never holds -0, so the +0 of the untouched cells'
+// selects is exact), without one dependent global round trip per event.
+template <int NB>
 __global__ __launch_bounds__(256) void v2e_emit_kernel(Call c, State s, Scratch w, const float *frames, float *vox,
                                                        int n, float dt_frame) {
-    const long long HW = (long long)c.H * c.W;
-    const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const int HW = c.H * c.W;
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
     const cista_v2e_config &g = c.cfg;
-    unsigned long long nev = 0;
-    if (i < (long long)c.B * HW) {
-        const int b = (int)(i / HW);
-        const long long p = i - b * HW;
+    unsigned nev = 0;
+    if (i < c.B * HW) {
+        const int b = i / HW;
+        const int p = i - b * HW;
+        // the per-pixel operands in one batch of loads (the voxel cells only at the first event)
+        const bool shot = g.shot_noise_rate_hz > 0.0f;
         const int cnt = w.counts[i];
         const float pol = w.pol[i];
-        const int max_iters = w.meta[0];
-        const bool refr = w.meta[1] != 0;
-        const int ni = w.num_iters[b];
-        const float step = w.ts_step[b];
-        const float Tr = c.Tr[b];
-        const float C = (pol > 0.0f ? s.pos[i] : 0.0f) + (pol < 0.0f ? s.neg[i] : 0.0f);
-        // shot noise thresholds (generate_shot_noise, emulator_utils.py:159-207)
-        float on_thr = 1.0f, off_thr = 0.0f;
-        const bool shot = g.shot_noise_rate_hz > 0.0f && pol != 0.0f;
-        if (shot) {
-            const float inten = rescale(frames[((long long)b * c.F + n) * HW + p]);
-            const float factor = (g.shot_noise_rate_hz / 2.0f * dt_frame / (float)ni) * ((0.25f - 1.0f) * inten + 1.0f);
-            on_thr = 1.0f - factor * s.pos_pre[i];
-            off_thr = factor * s.neg_pre[i];
-        }
-        float tmem = s.tmem[i];
+        const float pos = s.pos[i], neg = s.neg[i], base = s.base[i], tmem0 = s.tmem[i];
+        const float fr = shot ? frames[((size_t)b * c.F + n) * HW + p] : 0.0f;
+        const float pos_pre = shot ? s.pos_pre[i] : 0.0f, neg_pre = shot ? s.neg_pre[i] : 0.0f;
+        const float C = (pol > 0.0f ? pos : 0.0f) + (pol < 0.0f ? neg : 0.0f);
         int final_cnt = 0;
-        float *vp = vox + (size_t)b * c.nb * HW + p;
-        const float t0 = c.time_frames[n - 1];
-        for (int it = 0; it < max_iters; ++it) {
-            bool m = cnt >= it + 1;                            // :459
-            if (shot && it < ni) {                             // num_iter_mask (:196-198)
-                const float r = rand01(c.seed, c.draw0 + 9 + 2 * (unsigned long long)n,
-                                       ((unsigned long long)it * c.B + b) * HW + p);
-                m = m || (pol > 0.0f ? r > on_thr : r < off_thr);
+        if (pol != 0.0f) {                 // pol == 0: no count, no shot noise, no event (exact skip)
+            const int max_iters = w.meta[0];
+            const bool refr = w.meta[1] != 0;
+            const int ni = w.num_iters[b];
+            const float step = w.ts_step[b];
+            const float Tr = c.Tr[b];
+            const int nb = c.nb;
+            // shot noise thresholds (generate_shot_noise, emulator_utils.py:159-207)
+            float on_thr = 1.0f, off_thr = 0.0f;
+            if (shot) {
+                const float inten = rescale(fr);
+                const float factor = (g.shot_noise_rate_hz / 2.0f * dt_frame / (float)ni) * ((0.25f - 1.0f) * inten + 1.0f);
+                on_thr = 1.0f - factor * pos_pre;
+                off_thr = factor * neg_pre;
             }
-            const float ts = it < ni ? t0 + step * (float)(it + 1) : 0.0f;   // :428-432
-            if (refr) {                                        // :469-473
-                const float since = ts * (m ? 1.0f : 0.0f) - tmem;
-                m = since > Tr;
-                if (m) tmem = ts;
+            float tmem = tmem0;
+            float *vp = vox + (size_t)b * nb * HW + p;
+            const float t0 = c.time_frames[n - 1];
+            float cell[NB];
+            unsigned touched = 0;
+            bool loaded = false;
+            U4 rq{0u, 0u, 0u, 0u};                         // the 4 uniforms of iterations 4q .. 4q+3
+            int q_have = -1;
+            for (int it = 0; it < max_iters; ++it) {
+                bool m = cnt >= it + 1;                        // :459
+                // num_iter_mask (:196-198); the draw only matters when the count has not already
+                // set the mask (mask = count OR shot).  One Philox block serves 4 iterations.
+                if (shot && it < ni && !m) {
+                    const int q = it >> 2;
+                    if (q != q_have) {
+                        rq = draw(c.seed, c.draw0 + 9 + 2 * (unsigned long long)n,
+                                  ((unsigned long long)q * c.B + b) * HW + p);
+                        q_have = q;
+                    }
+                    const unsigned u = (it & 3) == 0 ? rq.x : (it & 3) == 1 ? rq.y : (it & 3) == 2 ? rq.z : rq.w;
+                    const float r = u01(u);
+                    m = pol > 0.0f ? r > on_thr : r < off_thr;
+                }
+                const float ts = it < ni ? t0 + step * (float)(it + 1) : 0.0f;   // :428-432
+                if (refr) {                                    // :469-473
+                    const float since = ts * (m ? 1.0f : 0.0f) - tmem;
+                    m = since > Tr;
+                    if (m) tmem = ts;
+                }
+                if (!m) continue;
+                final_cnt += 1;                                // :476
+                const float ti = floorf(ts);                   // :479-484
+                const float dts = ts - ti;
+                if (ti >= 0.0f) {
+                    if (!loaded) {
+#pragma unroll
+                        for (int j = 0; j < NB; ++j) cell[j] = j < nb ? vp[(size_t)j * HW] : 0.0f;
+                        loaded = true;
+                    }
+                    const int k = (int)ts;
+                    nev += 1;
+                    const float vl = pol * (1.0f - dts), vr = pol * dts;
+                    const bool right = ti + 1.0f < (float)nb;
+#pragma unroll
+                    for (int j = 0; j < NB; ++j) {             // k >= nb: dropped
+                        if (j == k) cell[j] += vl;
+                        if (j == k + 1 && right) cell[j] += vr;
+                    }
+                    if (k < nb) touched |= 1u << k;
+                    if (right) touched |= 1u << (k + 1);
+                }
             }
-            if (!m) continue;
-            final_cnt += 1;                                    // :476
-            const float ti = floorf(ts);                       // :479-484
-            const float dts = ts - ti;
-            if (ti >= 0.0f) {
-                const int k = (int)ts;
-                nev += 1;
-                if (k < c.nb) vp[(size_t)k * HW] += pol * (1.0f - dts);   // k >= nb: dropped
-                if (ti + 1.0f < (float)c.nb) vp[(size_t)(k + 1) * HW] += pol * dts;
-            }
+#pragma unroll
+            for (int j = 0; j < NB; ++j)
+                if ((touched >> j) & 1u) vp[(size_t)j * HW] = cell[j];
+            if (refr) s.tmem[i] = tmem;
         }
-        if (refr) s.tmem[i] = tmem;
-        s.base[i] = s.base[i] + pol * (float)final_cnt * C;   // :520
+        s.base[i] = base + pol * (float)final_cnt * C;        // :520
     }
-    // events generated: block reduction then one atomic
-    __shared__ unsigned long long red[256];
-    red[threadIdx.x] = nev;
+    // events generated: wave sums, then one atomic per workgroup
+    __shared__ unsigned red[4];
+    unsigned t = nev;
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = t;
     __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
-        __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned long long tot = (unsigned long long)red[0] + red[1] + red[2] + red[3];
+        // slot per workgroup: thousands of same-address atomics serialise in L2 (~10 ns each:
+        // 3600 of them were the whole 39 us of this kernel at 720x1280)
+        if (tot) atomicAdd(w.nev + (blockIdx.x % MAXSLOTS) * (SLOTW / 2), tot);
     }
-    if (threadIdx.x == 0 && red[0]) atomicAdd(w.nev, red[0]);
+}
+
+__global__ void v2e_nev_kernel(Scratch w, unsigned long long *out) {
+    unsigned long long t = w.nev[threadIdx.x * (SLOTW / 2)];   // 64 lanes = MAXSLOTS slots
+    for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+    if (threadIdx.x == 0) *out = t;
 }
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -325,11 +394,11 @@ WsLayout carve_ws(void *base, int B, int H, int W, int nb) {
     };
     L.sc.counts = static_cast<int *>(take(n * 4));
     L.sc.pol = static_cast<float *>(take(n * 4));
-    L.sc.iters_raw = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * MAXSLOTS * 4));
+    L.sc.iters_raw = static_cast<int *>(take((size_t)CISTA_V2E_MAX_BATCH * MAXSLOTS * SLOTW * 4));
     L.sc.num_iters = static_cast<int *>(take(CISTA_V2E_MAX_BATCH * 4));
     L.sc.ts_step = static_cast<float *>(take(CISTA_V2E_MAX_BATCH * 4));
     L.sc.meta = static_cast<int *>(take(16));
-    L.sc.nev = static_cast<unsigned long long *>(take(8));
+    L.sc.nev = static_cast<unsigned long long *>(take(MAXSLOTS * SLOTW * 4));
     L.vox_ws_bytes = cista_voxel_workspace_bytes(1, 0, B * nb, H, W);
     L.vox_ws = take(L.vox_ws_bytes);
     L.bytes = off;
@@ -405,6 +474,7 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
     }
     c.linlog_f = (1.0 / 20.0) * log(20.0);
     const long long npx = (long long)B * H * W;
+    if (npx >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;                          // 32-bit pixel index
 
     if (!hs->initialized) {
         c.draw0 = hs->draw;
@@ -417,19 +487,22 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
     }
     if (!(c.tf[1] > hs->t_previous)) return CISTA_ERR_INVALID;                     // :339-342
     if (hipMemsetAsync(voxels, 0, (size_t)B * nb * H * W * 4, st) != hipSuccess) return CISTA_ERR_HIP;
-    if (hipMemsetAsync(L.sc.nev, 0, 8, st) != hipSuccess) return CISTA_ERR_HIP;
+    if (hipMemsetAsync(L.sc.nev, 0, MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     c.draw0 = hs->draw;
     hs->draw += 2 * (unsigned long long)F + 16;
+    // the image-max slots start cleared; each frame's v2e_iters_kernel clears them after reading
+    if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     for (int n = 1; n < F; ++n) {
         const float dt = c.tf[n] - hs->t_previous;                                 // :352
-        if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * MAXSLOTS * 4, st) != hipSuccess) return CISTA_ERR_HIP;
         hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
         hipLaunchKernelGGL(v2e_iters_kernel, dim3(1), dim3(64), 0, st, c, L.sc);
-        hipLaunchKernelGGL(v2e_emit_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, voxels, n, dt);
+        if (nb <= 5)
+            hipLaunchKernelGGL(v2e_emit_kernel<5>, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, voxels, n, dt);
+        else
+            hipLaunchKernelGGL(v2e_emit_kernel<16>, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, voxels, n, dt);
         hs->t_previous = c.tf[n];                                                  // :518
     }
-    if (num_events && hipMemcpyAsync(num_events, L.sc.nev, 8, hipMemcpyDeviceToDevice, st) != hipSuccess)
-        return CISTA_ERR_HIP;
+    if (num_events) hipLaunchKernelGGL(v2e_nev_kernel, dim3(1), dim3(MAXSLOTS), 0, st, L.sc, num_events);
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     // event_preprocess_pytorch(mode='std', filter_hot_pixel=False) over the whole tensor (:526)
     return cista_voxel_preprocess(voxels, 1, B * nb, H, W, CISTA_VOXEL_STD_F32, 0.0f, L.vox_ws, L.vox_ws_bytes,

@@ -698,7 +698,6 @@ __global__ __launch_bounds__(256) void vox_stats_kernel(const ChunkPart *parts, 
     __shared__ ChunkPart sp[SBATCH];
     const int b = blockIdx.x;
     float s = 0.0f, q = 0.0f, mn = INFINITY, mx = -INFINITY;
-    double sd = 0.0, qd = 0.0;
     long long nnz = 0;
     for (int c0 = 0; c0 < nchunks; c0 += SBATCH) {
         const int nc = min(SBATCH, nchunks - c0);
@@ -710,8 +709,6 @@ __global__ __launch_bounds__(256) void vox_stats_kernel(const ChunkPart *parts, 
                 const ChunkPart p = sp[c];
                 s += p.sum;
                 q += p.sq;
-                sd += (double)p.sum;
-                qd += (double)p.sq;
                 nnz += p.nnz;
                 mn = fminf(mn, p.mn);
                 mx = fmaxf(mx, p.mx);
@@ -721,16 +718,7 @@ __global__ __launch_bounds__(256) void vox_stats_kernel(const ChunkPart *parts, 
     WinStats w;
     w.nnz = nnz; w.mn = mn; w.mx = mx;
     w.mean = 0.0; w.std = 0.0;
-    if (nnz > 0 && mode == CISTA_VOXEL_STD_F32) {
-        // event_preprocess_pytorch (:168-175): float32 scalars throughout.  The sums are taken
-        // in float64 over the chunk partials and rounded once (ATen's float32 reduction order is
-        // not restated; the difference is the last bit of sum())
-        const float nf = (float)nnz;
-        const float mean = (float)sd / nf;                   // sum() / num_nonzeros
-        const float var = (float)qd / nf - mean * mean;      // (v ** 2).sum() / n - mean ** 2
-        w.mean = mean;
-        w.std = sqrtf(var);
-    } else if (nnz > 0) {
+    if (nnz > 0 && mode == CISTA_VOXEL_STD) {
         const double dn = (double)nnz;
         const double mean = (double)s / dn;                  // :148
         w.mean = mean;
@@ -779,6 +767,92 @@ __global__ void vox_apply_kernel(float *vox, long long n, int mode, float thr, c
     }
 }
 
+// ---- CISTA_VOXEL_STD_F32 statistics: every element's v and float32(v * v) summed in float64 in a
+// fixed order (a workgroup per (block, window), then one per window), rounded once to float32
+// as the mode states.  Unlike the numpy modes there is no float32 pairwise order to reproduce,
+// so the whole grid streams at HBM rate instead of 8192-element chunks with serial tree walks.
+struct Part64 {
+    double s, q;
+    long long nnz;
+};
+
+inline int nblk64(long long n) {
+    const long long b = (n + 4095) / 4096;               // >= 16 elements per thread
+    return (int)(b < 1 ? 1 : b > 512 ? 512 : b);
+}
+
+__device__ __forceinline__ void acc64(float v0, float thr, double &s, double &q, int &nz) {
+    const float v = hot(v0, thr);
+    s += (double)v;
+    q += (double)(v * v);                                 // (v ** 2) in float32, then summed
+    nz += v != 0.0f;
+}
+
+// grid (nblk, B), block 256; thread t of block k takes float4 groups t + 256 (k + nblk j)
+__global__ __launch_bounds__(256) void vox_sum64_kernel(const float *vox, long long n, float thr, Part64 *parts) {
+    const int b = blockIdx.y, nblk = gridDim.x;
+    const float *a = vox + (size_t)b * n;
+    double s = 0.0, q = 0.0;
+    int nz = 0;
+    const bool al = (((size_t)a) & 15) == 0;
+    const long long n4 = al ? n / 4 : 0;
+    for (long long k = (long long)blockIdx.x * 256 + threadIdx.x; k < n4; k += (long long)nblk * 256) {
+        const float4 v = reinterpret_cast<const float4 *>(a)[k];
+        acc64(v.x, thr, s, q, nz); acc64(v.y, thr, s, q, nz);
+        acc64(v.z, thr, s, q, nz); acc64(v.w, thr, s, q, nz);
+    }
+    for (long long k = 4 * n4 + (long long)blockIdx.x * 256 + threadIdx.x; k < n; k += (long long)nblk * 256)
+        acc64(a[k], thr, s, q, nz);
+    __shared__ double ss[256], sq[256];
+    __shared__ long long sn[256];
+    ss[threadIdx.x] = s; sq[threadIdx.x] = q; sn[threadIdx.x] = nz;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            ss[threadIdx.x] += ss[threadIdx.x + k];
+            sq[threadIdx.x] += sq[threadIdx.x + k];
+            sn[threadIdx.x] += sn[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) parts[(size_t)b * nblk + blockIdx.x] = Part64{ss[0], sq[0], sn[0]};
+}
+
+// grid B, block 256: the window's block partials in a fixed tree, then the float32 statistics
+__global__ __launch_bounds__(256) void vox_stats64_kernel(const Part64 *parts, int nblk, WinStats *st) {
+    const int b = blockIdx.x;
+    double s = 0.0, q = 0.0;
+    long long nz = 0;
+    for (int k = threadIdx.x; k < nblk; k += 256) {
+        const Part64 p = parts[(size_t)b * nblk + k];
+        s += p.s; q += p.q; nz += p.nnz;
+    }
+    __shared__ double ss[256], sq[256];
+    __shared__ long long sn[256];
+    ss[threadIdx.x] = s; sq[threadIdx.x] = q; sn[threadIdx.x] = nz;
+    __syncthreads();
+    for (int k = 128; k > 0; k >>= 1) {
+        if ((int)threadIdx.x < k) {
+            ss[threadIdx.x] += ss[threadIdx.x + k];
+            sq[threadIdx.x] += sq[threadIdx.x + k];
+            sn[threadIdx.x] += sn[threadIdx.x + k];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x != 0) return;
+    WinStats w;
+    w.nnz = sn[0]; w.mn = 0.0f; w.mx = 0.0f;
+    w.mean = 0.0; w.std = 0.0;
+    if (w.nnz > 0) {                                     // event_preprocess_pytorch (:168-175)
+        const float nf = (float)w.nnz;
+        const float mean = (float)ss[0] / nf;                // sum() / num_nonzeros
+        const float var = (float)sq[0] / nf - mean * mean;   // (v ** 2).sum() / n - mean ** 2
+        w.mean = mean;
+        w.std = sqrtf(var);
+    }
+    st[b] = w;
+}
+
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
 
 struct VoxWs {
@@ -787,6 +861,7 @@ struct VoxWs {
     int *tb;                 // per-window tile starts of the sort + tile path
     void *tps;               // (t, polarity) of every event in sorted order (same path)
     ChunkPart *parts;
+    Part64 *parts64;         // CISTA_VOXEL_STD_F32 block partials
     WinStats *stats;
     void *cub;
     size_t cub_bytes, bytes;
@@ -818,6 +893,7 @@ VoxWs carve(void *base, int B, long long N, int nb, int H, int W) {
     w.tps = take(NN * 16);
     w.parts = static_cast<ChunkPart *>(take((size_t)(B > 0 ? B : 1) * nchunks * sizeof(ChunkPart)));
     w.stats = static_cast<WinStats *>(take((size_t)(B > 0 ? B : 1) * sizeof(WinStats)));
+    w.parts64 = static_cast<Part64 *>(take((size_t)(B > 0 ? B : 1) * nblk64(n) * sizeof(Part64)));
     w.cub_bytes = 0;
     if (N > 0) {
         const hipError_t e = hipcub::DeviceRadixSort::SortPairs(
@@ -849,7 +925,12 @@ bool big_lds(const void *kern) {
 // hot-pixel filter + normalisation of B grids of n floats, in place
 int preprocess(float *voxels, int B, long long n, int mode, float thr, const VoxWs &w, hipStream_t st) {
     const int nchunks = (int)((n + CHUNK - 1) / CHUNK);
-    if (mode != CISTA_VOXEL_RAW) {
+    if (mode == CISTA_VOXEL_STD_F32) {
+        const int nb64 = nblk64(n);
+        hipLaunchKernelGGL(vox_sum64_kernel, dim3(nb64, B), dim3(256), 0, st, (const float *)voxels, n, thr,
+                           w.parts64);
+        hipLaunchKernelGGL(vox_stats64_kernel, dim3(B), dim3(256), 0, st, (const Part64 *)w.parts64, nb64, w.stats);
+    } else if (mode != CISTA_VOXEL_RAW) {
         hipLaunchKernelGGL(vox_chunk_kernel, dim3(nchunks, B), dim3(MAX_LEAVES), 0, st, (const float *)voxels, n,
                            nchunks, thr, w.parts);
         hipLaunchKernelGGL(vox_stats_kernel, dim3(B), dim3(256), 0, st, (const ChunkPart *)w.parts, nchunks, mode,
