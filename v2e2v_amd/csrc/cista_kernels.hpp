@@ -1518,10 +1518,52 @@ __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) 
     const int cx0 = rowseg ? a0 : c0, ncx = rowseg ? a1 - a0 + 1 : c1 - c0 + 1;
     const int pitch = ncx | 1;
     const float *ev = a.events + (size_t)b * NB * plane, *im = a.prev + (size_t)b * plane;
-    for (int i = threadIdx.x; i < K * nry * ncx; i += 256) {      // column fastest: coalesced rows
-        const int x = i % ncx, r = (i / ncx) % nry, ci = i / (ncx * nry);
-        const float *src = ci < NB ? ev + (size_t)ci * plane : im;
-        strip[(ci * nry + r) * pitch + x] = src[(size_t)(ry0 + r) * W + cx0 + x];
+    // column fastest: coalesced rows; 8 loads in flight per thread before the LDS stores (a
+    // load-store pair per iteration waited a whole memory round trip 30 times per thread)
+    constexpr int SB = 8;
+    const int nstrip = K * nry * ncx;
+    for (int i0 = threadIdx.x; i0 < nstrip; i0 += 256 * SB) {
+        float v[SB];
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int i = i0 + u * 256;
+            v[u] = 0.0f;
+            if (i < nstrip) {
+                const int x = i % ncx, r = (i / ncx) % nry, ci = i / (ncx * nry);
+                const float *src = ci < NB ? ev + (size_t)ci * plane : im;
+                v[u] = src[(size_t)(ry0 + r) * W + cx0 + x];
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < SB; ++u) {
+            const int i = i0 + u * 256;
+            if (i < nstrip) {
+                const int x = i % ncx, r = (i / ncx) % nry, ci = i / (ncx * nry);
+                strip[(ci * nry + r) * pitch + x] = v[u];
+            }
+        }
+    }
+    // small batch (CT = 8): the class weights of the workgroup's 2 CT channels are staged in LDS
+    // too, [t][ci][2 CT], and read as broadcasts -- as scalar loads they were 25 dependent round
+    // trips per wave (one per tap), 33 us per 720x1280 frame
+    constexpr int WQ = 2 * CT;
+    __shared__ float wl[CT == 8 ? 25 * K * WQ : 1];
+    if constexpr (CT == 8) {
+        const float *Eg = a.E + (size_t)cls * 25 * K * C + blockIdx.y * WQ;
+        for (int i0 = threadIdx.x; i0 < 25 * K * WQ; i0 += 256 * SB) {
+            float v[SB];
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {      // clamped addresses: unconditional, batched loads
+                const int i = i0 + u * 256, ic = min(i, 25 * K * WQ - 1), j = ic % WQ, tc = ic / WQ;
+                const int jc = min((int)blockIdx.y * WQ + j, C - 1) - (int)blockIdx.y * WQ;
+                v[u] = Eg[(size_t)tc * C + jc];
+            }
+#pragma unroll
+            for (int u = 0; u < SB; ++u) {
+                const int i = i0 + u * 256;
+                if (i < 25 * K * WQ) wl[i] = (int)blockIdx.y * WQ + i % WQ < C ? v[u] : 0.0f;
+            }
+        }
     }
     __syncthreads();
     // strip-relative window position of tap t for output pixel (oy, ox); out-of-image window
@@ -1544,8 +1586,14 @@ __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) 
 #pragma unroll
             for (int ci = 0; ci < K; ++ci) {
                 const float vv = at(oy, ox, t, ci);
+                if constexpr (CT == 8) {
+                    const float *wr = wl + (t * K + ci) * WQ + (wave & 1) * CT;
 #pragma unroll
-                for (int i = 0; i < CT; ++i) acc[i] = fmaf(vv, wt[(size_t)ci * C + i], acc[i]);
+                    for (int i = 0; i < CT; ++i) acc[i] = fmaf(vv, wr[i], acc[i]);
+                } else {
+#pragma unroll
+                    for (int i = 0; i < CT; ++i) acc[i] = fmaf(vv, wt[(size_t)ci * C + i], acc[i]);
+                }
             }
         }
         if (chunk * 64 + lane < n) {
@@ -1562,9 +1610,17 @@ __global__ __launch_bounds__(256) void input_border_kernel(const FusedInArgs a) 
         const float *E = a.E + (size_t)ccls * 25 * K * C;
         for (int co = lane; co < C; co += 64) {
             float acc = a.bias[co];
-            for (int t = 0; t < 25; ++t)
+            // a window row's 5 K per-lane weights are loaded together, then used (5 round trips,
+            // not 25 K)
+            for (int ty = 0; ty < 5; ++ty) {
+                float wv[5 * K];
 #pragma unroll
-                for (int ci = 0; ci < K; ++ci) acc = fmaf(at(oy, ox, t, ci), E[((size_t)t * K + ci) * C + co], acc);
+                for (int k = 0; k < 5 * K; ++k) wv[k] = E[((size_t)(ty * 5) * K + k) * C + co];
+#pragma unroll
+                for (int tx = 0; tx < 5; ++tx)
+#pragma unroll
+                    for (int ci = 0; ci < K; ++ci) acc = fmaf(at(oy, ox, ty * 5 + tx, ci), wv[tx * K + ci], acc);
+            }
             a.out[(((size_t)b * h + oy) * w + ox) * C + co] = acc;
         }
     }
