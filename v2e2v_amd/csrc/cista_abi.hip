@@ -876,6 +876,10 @@ void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, flo
 #ifndef CISTA_WGRAD_SPLIT
 #define CISTA_WGRAD_SPLIT 1   // 0: every wgrad on the exact fp32-MFMA kernel (A/B builds)
 #endif
+#ifndef CISTA_WGRAD_TR
+#define CISTA_WGRAD_TR 1      // split-f16 wgrads on wgrad_tr_kernel (0: wgrad_split_kernel, A/B builds)
+#endif
+constexpr int NCU = 256;      // MI355X compute units (8 XCDs x 32)
 
 // dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor; and, when
 // db != NULL, db (+)= sign * (pixel sum of G) from the same pass over G (bias gradient).
@@ -898,8 +902,24 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.TH = WS_TH; a.TW = WS_TW;
         a.tiles_y = (Hout + WS_TH - 1) / WS_TH;
         a.tiles_x = (Wout + WS_TW - 1) / WS_TW;
-        const int nblk = (Cout / 64) * (Cin / 32);
         const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        if (CISTA_WGRAD_TR) {
+            // 64 x 64 blocks, one 8-wave workgroup per CU: splits fill the CUs once (and fit
+            // the partial buffer: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9)
+            const int nblk = (Cout / 64) * ((Cin + 63) / 64);
+            int ns = NCU / nblk;
+            const int lim = (int)(((long)WG_BLOCKS * 32 * 32) / ((long)Cout * Cin));
+            ns = ns > lim ? lim : ns;
+            ns = ns > ntiles ? ntiles : ns;
+            ns = ns < 1 ? 1 : ns;
+            ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
+            a.nsplit = ns;
+            if (!allow_big_lds((const void *)wgrad_tr_kernel)) return CISTA_ERR_HIP;
+            hipLaunchKernelGGL(wgrad_tr_kernel, dim3(nblk, ns), dim3(512), WT_LDS, k.st, a);
+            reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
+            return hip_ok();
+        }
+        const int nblk = (Cout / 64) * (Cin / 32);
         int ns = (WG_BLOCKS / 2) / nblk;   // partials: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9
         ns = ns > ntiles ? ntiles : ns;
         ns = ns < 1 ? 1 : ns;

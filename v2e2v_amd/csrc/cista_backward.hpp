@@ -587,6 +587,244 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
 }
 
 // --------------------------------------------------------------------------------------------
+// wgrad on split-f16 MFMA with transposed LDS reads (the default for the stride-1 NHWC convs with
+// 64-aligned Cout): dW[co][ci][t] = sum_P G(P, co) * Xpad(P + t, ci), per tap a (co x ci) GEMM
+// with K = pixels.  Workgroup = 64 co x 64 ci, 8 waves = 2 (32 co) x 4 (16 ci), 2 x 9
+// accumulators each; one workgroup per CU (two LDS buffers).
+//  * Both operands keep the natural channel-contiguous layout in LDS, as fp16 hi / lo planes of
+//    16 channels: plane[pixel][16 halves], 32 B per pixel.  The K (pixel) values of an MFMA
+//    fragment are gathered with gfx950's ds_read_b64_tr_b16 (lane 4q+p of a 16-lane group
+//    addresses pixel q, channels 4p..4p+3; lane i receives channel i of the 4 pixels), so a tap's
+//    shift is just another pixel address: the input halo is stored ONCE, not as the three
+//    column-shifted copies of wgrad_split_kernel (a third of its conversions and LDS stores).
+//  * K order of a 32-pixel K-step (tile rows 2s, 2s+1): lane group kg, read r covers pixels
+//    4kg..4kg+3 of row 2s+r, so a 32-lane half reads 8 consecutive pixels = 256 contiguous bytes
+//    of one plane (all 64 banks, conflict-free) for every tap shift.
+//  * Staging item (pixel, 4 channels): lanes 16k..16k+15 hold 4 pixels x 4 quads of plane k, so
+//    one pixel's 64 channels are one 256-B load run, and each ds_write_b64 lane group stores 128
+//    contiguous bytes (conflict-free).  The next tile's loads are issued before this tile's MFMAs
+//    and stored to the other buffer after them: one barrier per 96-pixel tile.
+//  * G is pre-scaled by the per-tensor power of two gscale[0] (exact).  X carries no per-tensor
+//    scale: every tile's X maximum rides on the tile's barrier; a tile whose |X| would overflow
+//    the fp16 hi part (>= 32768 after the scale in force) is re-staged with a smaller power-of-two
+//    pre-scale sx and the accumulators are rescaled exactly (rare path, uniform per workgroup).
+// --------------------------------------------------------------------------------------------
+constexpr int WT_NPX = 96, WT_HW = 18, WT_HP = 144;
+constexpr int WT_GPL = WT_NPX * 16;                 // halves per G plane (part, 16-co block)
+constexpr int WT_XPL = WT_HP * 16;                  // halves per X plane (part, 16-ci block)
+constexpr int WT_BUF = 8 * WT_GPL + 8 * WT_XPL;     // halves per buffer: G planes [2][4], X [2][4]
+constexpr size_t WT_LDS = (size_t)2 * WT_BUF * 2 + 2 * 8 * 4;   // + [2][8] per-wave X maxima
+
+typedef short s16x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
+
+// transposed read of 4 pixels x 16 channels of one plane (see above); off in halves, 8-B aligned
+__device__ __forceinline__ s16x4 tr_read(const _Float16 *sm, int off) {
+    return __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_s16x4 *)((__attribute__((address_space(3))) _Float16 *)sm + off));
+}
+
+__device__ __forceinline__ f16x8 cat_frag(const s16x4 &x0, const s16x4 &x1) {
+    typedef short s16x8 __attribute__((ext_vector_type(8)));
+    const s16x8 v = __builtin_shufflevector(x0, x1, 0, 1, 2, 3, 4, 5, 6, 7);
+    return __builtin_bit_cast(f16x8, v);
+}
+
+// 4 fp32 -> fp16 hi and lo (x ~= hi + lo), packed as 2 dwords each
+__device__ __forceinline__ void split4(const float4 &v, uint2 &hi, uint2 &lo) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+    const f2 v01 = {v.x, v.y}, v23 = {v.z, v.w};
+    const h2 h01 = __builtin_convertvector(v01, h2), h23 = __builtin_convertvector(v23, h2);
+    const f2 r01 = v01 - __builtin_convertvector(h01, f2), r23 = v23 - __builtin_convertvector(h23, f2);
+    hi = make_uint2(__builtin_bit_cast(unsigned, h01), __builtin_bit_cast(unsigned, h23));
+    lo = make_uint2(__builtin_bit_cast(unsigned, __builtin_convertvector(r01, h2)),
+                    __builtin_bit_cast(unsigned, __builtin_convertvector(r23, h2)));
+}
+
+__global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
+    extern __shared__ u32x4 wsm4[];
+    _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
+    float *xmx = reinterpret_cast<float *>(sm + 2 * WT_BUF);     // [2][8]
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ncb = (a.Cin + 63) / 64;
+    const int co0 = (blockIdx.x / ncb) * 64, ci0 = (blockIdx.x % ncb) * 64;
+    const int wcb = wave & 3;                  // the wave's 16-ci plane
+    const int wco = (wave >> 2) * 2;           // its first 16-co plane (two: wco, wco + 1)
+    const float gsc = a.gscale[0];
+    f32x4 acc[2][9];
+#pragma unroll
+    for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int t = 0; t < 9; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
+    float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    // staging roles: plane sb, pixel sp of a 4-pixel set, channel quad sq
+    const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
+    float4 gv[3], xv[5];
+    auto load_tile = [&](int tile) __attribute__((always_inline)) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * 6, ox0 = tx * 16;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int p = 4 * (wave + 8 * u) + sp;                       // 0..95
+            const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+            gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (oy < a.Hout && ox < a.Wout)
+                gv[u] = *reinterpret_cast<const float4 *>(
+                    a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int hp = 4 * (wave + 8 * u) + sp;                      // 0..159, valid < 144
+            const int hy = hp / WT_HW, hx = hp - hy * WT_HW;
+            xv[u] = hp < WT_HP ? wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq)
+                               : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto xmax_local = [&]() __attribute__((always_inline)) {
+        float m = 0.0f;
+#pragma unroll
+        for (int u = 0; u < 5; ++u)
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
+        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+        return m;
+    };
+    auto commit = [&](_Float16 *buf, float sx, bool bias) __attribute__((always_inline)) {
+        _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
+#pragma unroll
+        for (int u = 0; u < 3; ++u) {
+            const int p = 4 * (wave + 8 * u) + sp;
+            if (bias) { bsum.x += gv[u].x; bsum.y += gv[u].y; bsum.z += gv[u].z; bsum.w += gv[u].w; }
+            const float4 v = make_float4(gv[u].x * gsc, gv[u].y * gsc, gv[u].z * gsc, gv[u].w * gsc);
+            uint2 hi, lo;
+            split4(v, hi, lo);
+            *reinterpret_cast<uint2 *>(Gp + sb * WT_GPL + p * 16 + 4 * sq) = hi;
+            *reinterpret_cast<uint2 *>(Gp + (4 + sb) * WT_GPL + p * 16 + 4 * sq) = lo;
+        }
+#pragma unroll
+        for (int u = 0; u < 5; ++u) {
+            const int hp = 4 * (wave + 8 * u) + sp;
+            if (hp >= WT_HP) continue;
+            float4 v = xv[u];
+            if (__builtin_expect(sx != 1.0f, 0)) { v.x *= sx; v.y *= sx; v.z *= sx; v.w *= sx; }
+            uint2 hi, lo;
+            split4(v, hi, lo);
+            *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + hp * 16 + 4 * sq) = hi;
+            *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + hp * 16 + 4 * sq) = lo;
+        }
+    };
+    float sx = 1.0f;                            // X pre-scale in force (power of two, <= 1)
+    // after the barrier that published a tile's per-wave X maxima: re-stage it with a smaller
+    // pre-scale if its values overflowed the hi part (uniform: every wave reads the same maxima)
+    auto range_fix = [&](_Float16 *buf, const float *mx) __attribute__((always_inline)) {
+        float m = mx[0];
+#pragma unroll
+        for (int w = 1; w < 8; ++w) m = fmaxf(m, mx[w]);
+        if (__builtin_expect(m * sx >= 32768.0f && m < 3.0e38f, 0)) {
+            int e = (int)floorf(log2f(16384.0f / m));
+            e = e < -126 ? -126 : e;
+            const float st = ldexpf(1.0f, e);
+            const float r = st / sx;
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[u][t] *= r;
+            sx = st;
+            commit(buf, sx, false);
+            __syncthreads();
+        }
+    };
+    const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
+    int it = 0;
+    if ((int)blockIdx.y < ntiles) {
+        load_tile(blockIdx.y);
+        const float m = xmax_local();
+        if (lane == 0) xmx[wave] = m;
+        commit(sm, sx, do_bias);
+        __syncthreads();
+        range_fix(sm, xmx);
+    }
+    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
+        const _Float16 *cur = sm + (it & 1) * WT_BUF;
+        _Float16 *nxt = sm + ((it + 1) & 1) * WT_BUF;
+        const bool more = tile + a.nsplit < ntiles;
+        if (more) load_tile(tile + a.nsplit);
+        const _Float16 *Gp = cur, *Xp = cur + 8 * WT_GPL;
+#pragma unroll
+        for (int s = 0; s < 3; ++s) {
+            s16x4 ah[2][2], al[2][2];
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int off = (wco + u) * WT_GPL + ((2 * s + r) * 16 + 4 * kg + rq) * 16 + 4 * rp;
+                    ah[u][r] = tr_read(Gp, off);
+                    al[u][r] = tr_read(Gp, off + 4 * WT_GPL);
+                }
+#pragma unroll
+            for (int t = 0; t < 9; ++t) {
+                const int dy = t / 3, dx = t % 3;
+                s16x4 bh[2], bl[2];
+#pragma unroll
+                for (int r = 0; r < 2; ++r) {
+                    const int off = wcb * WT_XPL + ((2 * s + r + dy) * WT_HW + 4 * kg + rq + dx) * 16 + 4 * rp;
+                    bh[r] = tr_read(Xp, off);
+                    bl[r] = tr_read(Xp, off + 4 * WT_XPL);
+                }
+                const f16x8 xh = cat_frag(bh[0], bh[1]), xl = cat_frag(bl[0], bl[1]);
+#pragma unroll
+                for (int u = 0; u < 2; ++u) {
+                    const f16x8 gh = cat_frag(ah[u][0], ah[u][1]), gl = cat_frag(al[u][0], al[u][1]);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, xh, acc[u][t], 0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, xl, acc[u][t], 0, 0, 0);
+                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, xh, acc[u][t], 0, 0, 0);
+                }
+            }
+        }
+        if (more) {
+            const float m = xmax_local();
+            if (lane == 0) xmx[((it + 1) & 1) * 8 + wave] = m;
+            commit(nxt, sx, do_bias);
+        }
+        __syncthreads();
+        if (more) range_fix(nxt, xmx + ((it + 1) & 1) * 8);
+    }
+    if (do_bias) {
+        // thread sums of co quad 16 sb + 4 sq -> per-co sums in a fixed order (waves, then sp)
+        __syncthreads();
+        float4 *red = reinterpret_cast<float4 *>(wsm4);
+        red[tid] = bsum;
+        __syncthreads();
+        if (tid < 64) {
+            const int b16 = tid >> 4, q4 = (tid >> 2) & 3, e = tid & 3;
+            float t = 0.0f;
+            for (int w = 0; w < 8; ++w)
+                for (int p = 0; p < 4; ++p) t += (&red[64 * w + 16 * b16 + 4 * p + q4].x)[e];
+            a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + tid] = t;
+        }
+    }
+    // acc[u][t][j]: row (cout) 16 (wco + u) + 4 (lane >> 4) + j, col (cin) 16 wcb + (lane & 15)
+    const float inv = a.gscale[1] * (1.0f / sx);
+    float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
+    const int ci = ci0 + 16 * wcb + (lane & 15);
+    if (ci < a.Cin)
+#pragma unroll
+        for (int u = 0; u < 2; ++u)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {
+                const int co = co0 + 16 * (wco + u) + 4 * (lane >> 4) + j;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[u][t][j] * inv;
+            }
+}
+
+// --------------------------------------------------------------------------------------------
 // wgrad of a one-output-channel stride-1 conv (final_conv, 64 -> 1): dW[ci][t] = sum_P g(P) *
 // Xpad(P + t, ci) on VALU (an MFMA block would waste 31 of 32 rows).  blockIdx.x = 32-channel
 // block, blockIdx.y = split over 16 x 16 pixel tiles.  The reflect-padded 18 x 18 x 32 input
