@@ -613,7 +613,7 @@ constexpr int WT_NPX = 96, WT_HW = 18, WT_HP = 144;
 constexpr int WT_GPL = WT_NPX * 16;                 // halves per G plane (part, 16-co block)
 constexpr int WT_XPL = WT_HP * 16;                  // halves per X plane (part, 16-ci block)
 constexpr int WT_BUF = 8 * WT_GPL + 8 * WT_XPL;     // halves per buffer: G planes [2][4], X [2][4]
-constexpr size_t WT_LDS = (size_t)2 * WT_BUF * 2 + 2 * 8 * 4;   // + [2][8] per-wave X maxima
+constexpr size_t WT_LDS = (size_t)2 * WT_BUF * 2 + 16 * 4;      // + maxima, flags, scale
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -645,34 +645,43 @@ __device__ __forceinline__ void split4(const float4 &v, uint2 &hi, uint2 &lo) {
 __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
     _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
-    float *xmx = reinterpret_cast<float *>(sm + 2 * WT_BUF);     // [2][8]
+    float *xmx = reinterpret_cast<float *>(sm + 2 * WT_BUF);     // [4] loader X maxima (rare path)
+    int *xfl = reinterpret_cast<int *>(xmx + 4);                 // [2][4] per-buffer overflow flags
+    float *xsc = xmx + 12;                                       // [1] new X pre-scale (rare path)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ncb = (a.Cin + 63) / 64;
     const int co0 = (blockIdx.x / ncb) * 64, ci0 = (blockIdx.x % ncb) * 64;
-    const int wcb = wave & 3;                  // the wave's 16-ci plane
-    const int wco = (wave >> 2) * 2;           // its first 16-co plane (two: wco, wco + 1)
+    const bool loader = wave >= 4;             // waves 0-3: MFMAs; waves 4-7: staging
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
     const float gsc = a.gscale[0];
-    f32x4 acc[2][9];
-#pragma unroll
-    for (int u = 0; u < 2; ++u)
-#pragma unroll
-        for (int t = 0; t < 9; ++t) acc[u][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    float sx = 1.0f;                           // X pre-scale in force (power of two, <= 1)
+
+    // ---- staging (loader waves): item (pixel 4 set + sp, channel quad sq of plane sb) ----
+    const int lw = wave - 4;
+    const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
     const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
-    const int ntiles = a.B * a.tiles_y * a.tiles_x;
-    // staging roles: plane sb, pixel sp of a 4-pixel set, channel quad sq
-    const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
-    float4 gv[3], xv[5];
-    auto load_tile = [&](int tile) __attribute__((always_inline)) {
+    float4 gv[6], xv[9];
+    auto tile_origin = [&](int tile, int &b, int &oy0, int &ox0) __attribute__((always_inline)) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
         tt /= a.tiles_x;
         const int ty = tt % a.tiles_y;
-        const int b = tt / a.tiles_y;
-        const int oy0 = ty * 6, ox0 = tx * 16;
+        b = tt / a.tiles_y;
+        oy0 = ty * 6;
+        ox0 = tx * 16;
+    };
+    auto load_x = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
+        const int hp = 4 * (lw + 4 * u) + sp;                            // 0..143
+        const int hy = hp / WT_HW, hx = hp - hy * WT_HW;
+        return wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
+    };
+    auto load_tile = [&](int tile) __attribute__((always_inline)) {
+        int b, oy0, ox0;
+        tile_origin(tile, b, oy0, ox0);
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int p = 4 * (wave + 8 * u) + sp;                       // 0..95
+        for (int u = 0; u < 6; ++u) {
+            const int p = 4 * (lw + 4 * u) + sp;                         // 0..95
             const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
             gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (oy < a.Hout && ox < a.Wout)
@@ -680,148 +689,199 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                     a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
         }
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int hp = 4 * (wave + 8 * u) + sp;                      // 0..159, valid < 144
-            const int hy = hp / WT_HW, hx = hp - hy * WT_HW;
-            xv[u] = hp < WT_HP ? wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq)
-                               : make_float4(0.f, 0.f, 0.f, 0.f);
-        }
+        for (int u = 0; u < 9; ++u) xv[u] = load_x(b, oy0, ox0, u);
     };
-    auto xmax_local = [&]() __attribute__((always_inline)) {
-        float m = 0.0f;
-#pragma unroll
-        for (int u = 0; u < 5; ++u)
-            m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
-        for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-        return m;
+    auto put_x = [&](_Float16 *Xp, int u, float4 v) __attribute__((always_inline)) {
+        const int hp = 4 * (lw + 4 * u) + sp;
+        if (__builtin_expect(sx != 1.0f, 0)) { v.x *= sx; v.y *= sx; v.z *= sx; v.w *= sx; }
+        uint2 hi, lo;
+        split4(v, hi, lo);
+        *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + hp * 16 + 4 * sq) = hi;
+        *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + hp * 16 + 4 * sq) = lo;
     };
-    auto commit = [&](_Float16 *buf, float sx, bool bias) __attribute__((always_inline)) {
+    // registers -> LDS buffer (hi / lo planes); publishes whether this wave's X overflowed
+    auto commit = [&](_Float16 *buf, int *flag) __attribute__((always_inline)) {
         _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
 #pragma unroll
-        for (int u = 0; u < 3; ++u) {
-            const int p = 4 * (wave + 8 * u) + sp;
-            if (bias) { bsum.x += gv[u].x; bsum.y += gv[u].y; bsum.z += gv[u].z; bsum.w += gv[u].w; }
+        for (int u = 0; u < 6; ++u) {
+            const int p = 4 * (lw + 4 * u) + sp;
+            if (do_bias) { bsum.x += gv[u].x; bsum.y += gv[u].y; bsum.z += gv[u].z; bsum.w += gv[u].w; }
             const float4 v = make_float4(gv[u].x * gsc, gv[u].y * gsc, gv[u].z * gsc, gv[u].w * gsc);
             uint2 hi, lo;
             split4(v, hi, lo);
             *reinterpret_cast<uint2 *>(Gp + sb * WT_GPL + p * 16 + 4 * sq) = hi;
             *reinterpret_cast<uint2 *>(Gp + (4 + sb) * WT_GPL + p * 16 + 4 * sq) = lo;
         }
+        float m = 0.0f;
 #pragma unroll
-        for (int u = 0; u < 5; ++u) {
-            const int hp = 4 * (wave + 8 * u) + sp;
-            if (hp >= WT_HP) continue;
-            float4 v = xv[u];
-            if (__builtin_expect(sx != 1.0f, 0)) { v.x *= sx; v.y *= sx; v.z *= sx; v.w *= sx; }
-            uint2 hi, lo;
-            split4(v, hi, lo);
-            *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + hp * 16 + 4 * sq) = hi;
-            *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + hp * 16 + 4 * sq) = lo;
+        for (int u = 0; u < 9; ++u) {
+            m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
+            put_x(Xp, u, xv[u]);
         }
+        const bool ovf = m * sx >= 32768.0f && m < 3.0e38f;               // hi part would overflow
+        const bool any = __ballot(ovf ? 1 : 0) != 0;
+        if (lane == 0) flag[lw] = any ? 1 : 0;
     };
-    float sx = 1.0f;                            // X pre-scale in force (power of two, <= 1)
-    // after the barrier that published a tile's per-wave X maxima: re-stage it with a smaller
-    // pre-scale if its values overflowed the hi part (uniform: every wave reads the same maxima)
-    auto range_fix = [&](_Float16 *buf, const float *mx) __attribute__((always_inline)) {
-        float m = mx[0];
+    // rare path (uniform: every wave read the same flags): the tile in buf is re-staged with a
+    // smaller X pre-scale, the MFMA waves rescale their accumulators exactly.  The loaders re-read
+    // the tile's X one item at a time (their registers hold the next tile's loads in flight).
+    // Both roles pass the same three barriers and derive the same scale from the same maxima.
+    auto new_scale = [&]() __attribute__((always_inline)) {
+        const float m = fmaxf(fmaxf(xmx[0], xmx[1]), fmaxf(xmx[2], xmx[3]));
+        int e = (int)floorf(log2f(16384.0f / m));
+        e = e < -126 ? -126 : e;
+        const float st = fminf(ldexpf(1.0f, e), sx);
+        const float r = st / sx;
+        sx = st;
+        return r;
+    };
+    auto acc_zero = [](f32x4 (&acc)[2][2][9]) __attribute__((always_inline)) {
 #pragma unroll
-        for (int w = 1; w < 8; ++w) m = fmaxf(m, mx[w]);
-        if (__builtin_expect(m * sx >= 32768.0f && m < 3.0e38f, 0)) {
-            int e = (int)floorf(log2f(16384.0f / m));
-            e = e < -126 ? -126 : e;
-            const float st = ldexpf(1.0f, e);
-            const float r = st / sx;
+        for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int u = 0; u < 2; ++u)
+            for (int v = 0; v < 2; ++v)
 #pragma unroll
-                for (int t = 0; t < 9; ++t) acc[u][t] *= r;
-            sx = st;
-            commit(buf, sx, false);
+                for (int t = 0; t < 9; ++t) acc[u][v][t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    };
+    auto flagged = [&](int bi) __attribute__((always_inline)) {
+        return (xfl[4 * bi] | xfl[4 * bi + 1] | xfl[4 * bi + 2] | xfl[4 * bi + 3]) != 0;
+    };
+
+    if (loader) {
+        // the roles run separate loops with the same barrier sequence, so the loaders' staging
+        // registers and the MFMA waves' accumulators are never live at the same time
+        if ((int)blockIdx.y < ntiles) {
+            load_tile(blockIdx.y);
+            commit(sm, xfl);
+            if ((int)blockIdx.y + a.nsplit < ntiles) load_tile(blockIdx.y + a.nsplit);
+        }
+        __syncthreads();
+        int it = 0;
+        for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
+            const int bi = it & 1;
+            if (__builtin_expect(flagged(bi), 0)) {
+                __syncthreads();
+                int b, oy0, ox0;
+                tile_origin(tile, b, oy0, ox0);
+                float m = 0.0f;
+#pragma unroll 1
+                for (int u = 0; u < 9; ++u) {
+                    const float4 v = load_x(b, oy0, ox0, u);
+                    m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+                }
+                for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+                if (lane == 0) xmx[lw] = m;
+                __syncthreads();
+                new_scale();
+#pragma unroll 1
+                for (int u = 0; u < 9; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
+                __syncthreads();
+            }
+            if (tile + a.nsplit < ntiles) {
+                // the other buffer was last read before the barrier that opened this iteration
+                commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1));
+                if (tile + 2 * a.nsplit < ntiles) load_tile(tile + 2 * a.nsplit);
+            }
             __syncthreads();
         }
-    };
-    const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
-    int it = 0;
-    if ((int)blockIdx.y < ntiles) {
-        load_tile(blockIdx.y);
-        const float m = xmax_local();
-        if (lane == 0) xmx[wave] = m;
-        commit(sm, sx, do_bias);
-        __syncthreads();
-        range_fix(sm, xmx);
+        if (do_bias) {
+            reinterpret_cast<float4 *>(wsm4)[tid - 256] = bsum;
+            __syncthreads();
+        }
+        return;
     }
+
+    // ---- MFMA waves: 32 co (planes pco, pco + 1) x 32 ci (planes pci, pci + 1) ----
+    const int pco = 2 * (wave >> 1), pci = 2 * (wave & 1);
+    const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
+    f32x4 acc[2][2][9];
+    acc_zero(acc);
+    __syncthreads();
+    int it = 0;
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
-        const _Float16 *cur = sm + (it & 1) * WT_BUF;
-        _Float16 *nxt = sm + ((it + 1) & 1) * WT_BUF;
-        const bool more = tile + a.nsplit < ntiles;
-        if (more) load_tile(tile + a.nsplit);
-        const _Float16 *Gp = cur, *Xp = cur + 8 * WT_GPL;
-#pragma unroll
-        for (int s = 0; s < 3; ++s) {
-            s16x4 ah[2][2], al[2][2];
+        const int bi = it & 1;
+        if (__builtin_expect(flagged(bi), 0)) {
+            __syncthreads();
+            __syncthreads();
+            const float r = new_scale();
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const int off = (wco + u) * WT_GPL + ((2 * s + r) * 16 + 4 * kg + rq) * 16 + 4 * rp;
-                    ah[u][r] = tr_read(Gp, off);
-                    al[u][r] = tr_read(Gp, off + 4 * WT_GPL);
-                }
+                for (int v = 0; v < 2; ++v)
 #pragma unroll
-            for (int t = 0; t < 9; ++t) {
-                const int dy = t / 3, dx = t % 3;
-                s16x4 bh[2], bl[2];
-#pragma unroll
-                for (int r = 0; r < 2; ++r) {
-                    const int off = wcb * WT_XPL + ((2 * s + r + dy) * WT_HW + 4 * kg + rq + dx) * 16 + 4 * rp;
-                    bh[r] = tr_read(Xp, off);
-                    bl[r] = tr_read(Xp, off + 4 * WT_XPL);
-                }
-                const f16x8 xh = cat_frag(bh[0], bh[1]), xl = cat_frag(bl[0], bl[1]);
-#pragma unroll
-                for (int u = 0; u < 2; ++u) {
-                    const f16x8 gh = cat_frag(ah[u][0], ah[u][1]), gl = cat_frag(al[u][0], al[u][1]);
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, xh, acc[u][t], 0, 0, 0);
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh, xl, acc[u][t], 0, 0, 0);
-                    acc[u][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl, xh, acc[u][t], 0, 0, 0);
-                }
-            }
+                    for (int t = 0; t < 9; ++t) acc[u][v][t] *= r;
+            __syncthreads();
         }
-        if (more) {
-            const float m = xmax_local();
-            if (lane == 0) xmx[((it + 1) & 1) * 8 + wave] = m;
-            commit(nxt, sx, do_bias);
+        const _Float16 *Gp = sm + bi * WT_BUF, *Xp = Gp + 8 * WT_GPL;
+        // 27 (K-step, tap) steps, software-pipelined: the fragments of step n + 1 are read before
+        // step n's 12 MFMAs are issued, so their LDS latency hides under those MFMAs
+        auto read_g = [&](int s, f16x8 (&gh)[2], f16x8 (&gl)[2]) __attribute__((always_inline)) {
+#pragma unroll
+            for (int u = 0; u < 2; ++u) {
+                const int off = (pco + u) * WT_GPL + ((2 * s) * 16 + 4 * kg + rq) * 16 + 4 * rp;
+                gh[u] = cat_frag(tr_read(Gp, off), tr_read(Gp, off + 256));
+                gl[u] = cat_frag(tr_read(Gp, off + 4 * WT_GPL), tr_read(Gp, off + 4 * WT_GPL + 256));
+            }
+        };
+        auto read_x = [&](int s, int t, f16x8 (&xh)[2], f16x8 (&xl)[2]) __attribute__((always_inline)) {
+            const int dy = t / 3, dx = t % 3;
+#pragma unroll
+            for (int v = 0; v < 2; ++v) {
+                const int off = (pci + v) * WT_XPL + ((2 * s + dy) * WT_HW + 4 * kg + rq + dx) * 16 + 4 * rp;
+                xh[v] = cat_frag(tr_read(Xp, off), tr_read(Xp, off + WT_HW * 16));
+                xl[v] = cat_frag(tr_read(Xp, off + 4 * WT_XPL), tr_read(Xp, off + 4 * WT_XPL + WT_HW * 16));
+            }
+        };
+        f16x8 gh[2][2], gl[2][2], xh[2][2], xl[2][2];
+        read_g(0, gh[0], gl[0]);
+        read_x(0, 0, xh[0], xl[0]);
+#pragma unroll
+        for (int n = 0; n < 27; ++n) {
+            const int s = n / 9, t = n % 9, xb = n & 1, gb = s & 1;
+            if (n + 1 < 27) {
+                read_x((n + 1) / 9, (n + 1) % 9, xh[xb ^ 1], xl[xb ^ 1]);
+                if (t == 8) read_g(s + 1, gh[gb ^ 1], gl[gb ^ 1]);
+            }
+#pragma unroll
+            for (int u = 0; u < 2; ++u)
+#pragma unroll
+                for (int v = 0; v < 2; ++v) {
+                    acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh[gb][u], xh[xb][v], acc[u][v][t], 0, 0, 0);
+                    acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh[gb][u], xl[xb][v], acc[u][v][t], 0, 0, 0);
+                    acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl[gb][u], xh[xb][v], acc[u][v][t], 0, 0, 0);
+                }
+            __builtin_amdgcn_sched_barrier(0);
         }
         __syncthreads();
-        if (more) range_fix(nxt, xmx + ((it + 1) & 1) * 8);
     }
     if (do_bias) {
-        // thread sums of co quad 16 sb + 4 sq -> per-co sums in a fixed order (waves, then sp)
-        __syncthreads();
-        float4 *red = reinterpret_cast<float4 *>(wsm4);
-        red[tid] = bsum;
+        // loader sums of co quad 16 sb + 4 sq -> per-co sums in a fixed order (waves, then sp)
         __syncthreads();
         if (tid < 64) {
+            const float4 *red = reinterpret_cast<const float4 *>(wsm4);
             const int b16 = tid >> 4, q4 = (tid >> 2) & 3, e = tid & 3;
             float t = 0.0f;
-            for (int w = 0; w < 8; ++w)
+            for (int w = 0; w < 4; ++w)
                 for (int p = 0; p < 4; ++p) t += (&red[64 * w + 16 * b16 + 4 * p + q4].x)[e];
             a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + tid] = t;
         }
     }
-    // acc[u][t][j]: row (cout) 16 (wco + u) + 4 (lane >> 4) + j, col (cin) 16 wcb + (lane & 15)
+    // acc[u][v][t][j]: row (cout) 16 (pco + u) + 4 (lane >> 4) + j, col (cin) 16 (pci + v) + (lane & 15)
     const float inv = a.gscale[1] * (1.0f / sx);
     float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
-    const int ci = ci0 + 16 * wcb + (lane & 15);
-    if (ci < a.Cin)
+#pragma unroll
+    for (int v = 0; v < 2; ++v) {
+        const int ci = ci0 + 16 * (pci + v) + (lane & 15);
+        if (ci >= a.Cin) continue;
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
             for (int j = 0; j < 4; ++j) {
-                const int co = co0 + 16 * (wco + u) + 4 * (lane >> 4) + j;
+                const int co = co0 + 16 * (pco + u) + 4 * (lane >> 4) + j;
 #pragma unroll
-                for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[u][t][j] * inv;
+                for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[u][v][t][j] * inv;
             }
+    }
 }
 
 // --------------------------------------------------------------------------------------------
