@@ -732,15 +732,13 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
 #ifndef CISTA_WG_BLOCKS
 #define CISTA_WG_BLOCKS 1024
 #endif
-constexpr int ABS_BLOCKS = 256;              // workgroups of absmax_scale_kernel
 constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
     float *part, *bpart, *dlp;
     float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
-    unsigned *amax;     // [8] tickets of the gradient-scale kernel (zero between uses)
-    float *amax_part;   // [ABS_BLOCKS] its per-workgroup maxima
+    unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses)
     float *scl;         // [16] scale pairs
     size_t bytes;
 };
@@ -774,8 +772,7 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.bpart = take((size_t)WG_BLOCKS * 4 * C);
     s.dlp = take((size_t)2 * C * 512);
     s.wT = take((size_t)9 * C * C);
-    s.amax = reinterpret_cast<unsigned *>(take(16));
-    s.amax_part = take(ABS_BLOCKS);
+    s.amax = reinterpret_cast<unsigned *>(take((size_t)8 * AMAX_SLOTS * AMAX_STRIDE));
     s.scl = take(32);
     s.bytes = off;
     return s;
@@ -794,52 +791,16 @@ __device__ __forceinline__ void scale_from_max(float mx, float *scl) {
     scl[1] = ldexpf(1.0f, -e);
 }
 
-// max |x| and the scale in one launch: float4 grid-stride loads (4 in flight per thread), wave +
-// workgroup reduction, the workgroup maximum stored to part[blockIdx]; the last workgroup to
-// finish (one ticket atomic per workgroup: same-address atomics serialise, so the grid is kept
-// at ABS_BLOCKS) reduces the partial maxima, writes the scale and re-zeroes its ticket (the
-// backward zeroes all tickets once per call).  Replaces memset + absmax + a 1-thread scale
-// kernel (4.7 + 22.9 + 4.8 us per gradient tensor at B = 8).
-__global__ __launch_bounds__(256) void absmax_scale_kernel(const float *x, long n, unsigned *ticket, float *part,
-                                                           float *scl) {
+// {s, 1/s} from the |max| slots a producing kernel filled (amax_publish), slots re-zeroed
+__global__ __launch_bounds__(256) void slots_scale_kernel(unsigned *slots, float *scl) {
     __shared__ float red[4];
-    __shared__ bool last;
-    float m0 = 0.0f, m1 = 0.0f, m2 = 0.0f, m3 = 0.0f;
-    const long n4 = ((reinterpret_cast<uintptr_t>(x) & 15) == 0) ? n / 4 : 0;
-    const float4 *x4 = reinterpret_cast<const float4 *>(x);
-    const long stride = (long)gridDim.x * 256;
-    auto amax4 = [](float m, const float4 v) {
-        return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-    };
-    long i = (long)blockIdx.x * 256 + threadIdx.x;
-    for (; i + 3 * stride < n4; i += 4 * stride) {
-        const float4 v0 = x4[i], v1 = x4[i + stride], v2 = x4[i + 2 * stride], v3 = x4[i + 3 * stride];
-        m0 = amax4(m0, v0); m1 = amax4(m1, v1); m2 = amax4(m2, v2); m3 = amax4(m3, v3);
-    }
-    for (; i < n4; i += stride) m0 = amax4(m0, x4[i]);
-    for (long j = 4 * n4 + (long)blockIdx.x * 256 + threadIdx.x; j < n; j += stride) m0 = fmaxf(m0, fabsf(x[j]));
-    // fmaxf drops NaN (as the previous absmax did); an inf maximum gives the scale 1
-    float m = fmaxf(fmaxf(m0, m1), fmaxf(m2, m3));
+    const unsigned u = slots[threadIdx.x * AMAX_STRIDE];
+    slots[threadIdx.x * AMAX_STRIDE] = 0u;
+    float m = __uint_as_float(u);
     for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
     __syncthreads();
-    if (threadIdx.x == 0) {
-        part[blockIdx.x] = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
-        __threadfence();
-        last = atomicAdd(ticket, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();
-    float v = 0.0f;
-    for (int k = threadIdx.x; k < (int)gridDim.x; k += 256) v = fmaxf(v, __builtin_nontemporal_load(part + k));
-    for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o));
-    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = v;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        scale_from_max(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), scl);
-        atomicExch(ticket, 0u);
-    }
+    if (threadIdx.x == 0) scale_from_max(fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3])), scl);
 }
 
 struct Bwd {
@@ -854,15 +815,31 @@ struct Bwd {
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
 
-// per-tensor power-of-two scale {s, 1/s} of an output gradient G (n floats) for its fp16
-// splits (split-f16 dgrad and wgrad), in a rotating slot of the backward workspace
+// per-tensor power-of-two scale {s, 1/s} of an output gradient for its fp16 splits (split-f16
+// dgrad and wgrad), in a rotating slot of the backward workspace: the kernel that produces the
+// gradient is launched with scale_slots(k) and publishes its |max| there; scale_of then turns
+// the slots into the scale pair (one 256-thread launch)
+unsigned *scale_slots(Bwd &k, int ahead = 0) {
+    return k.ws.amax + (size_t)((k.slot + ahead) & 7) * AMAX_SLOTS * AMAX_STRIDE;
+}
+// a gradient whose producer does not publish: one grid-stride |max| pass into the slots
+__global__ __launch_bounds__(256) void absmax_publish_kernel(const float *x, long n, unsigned *slots) {
+    float m = 0.0f;
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
+    amax_publish(slots, m);
+}
+const float *scale_of(Bwd &k);
 const float *grad_scale(Bwd &k, const float *G, long n) {
-    unsigned *tk = k.ws.amax + (k.slot & 7);               // ticket, zero between uses
+    const long blocks = (n + 255) / 256;
+    hipLaunchKernelGGL(absmax_publish_kernel, dim3((unsigned)(blocks < 1 ? 1 : blocks > 1024 ? 1024 : blocks)), dim3(256),
+                       0, k.st, G, n, scale_slots(k));
+    return scale_of(k);
+}
+const float *scale_of(Bwd &k) {
+    unsigned *sl = scale_slots(k);
     float *sc = k.ws.scl + 2 * (k.slot & 7);
     ++k.slot;
-    const long blocks = (n / 4 + 255) / 256;
-    hipLaunchKernelGGL(absmax_scale_kernel, dim3((unsigned)(blocks < 1 ? 1 : blocks > ABS_BLOCKS ? ABS_BLOCKS : blocks)),
-                       dim3(256), 0, k.st, G, n, tk, k.ws.amax_part, sc);
+    hipLaunchKernelGGL(slots_scale_kernel, dim3(1), dim3(AMAX_SLOTS), 0, k.st, sl, sc);
     return hipGetLastError() == hipSuccess ? sc : nullptr;
 }
 
@@ -1024,11 +1001,12 @@ int dgrad_conv(Bwd &k, int id, const float *G, float *dxp, const float *sc = nul
 // add: dst = add + fold (copy-free identity path; NULL add with accumulate 0 is plain dst = fold);
 // dst2: a second destination receiving dst2 += fold from the same pass over src
 int fold(Bwd &k, const float *src, int Cs, int sc0, float *dst, int Cd, int dc0, int n, int H, int W,
-         float scale, int accumulate, const float *mask, const float *add = nullptr, float *dst2 = nullptr) {
+         float scale, int accumulate, const float *mask, const float *add = nullptr, float *dst2 = nullptr,
+         unsigned *amax = nullptr) {
     FoldArgs f;
     f.src = src; f.Cs = Cs; f.sc0 = sc0; f.dst = dst; f.Cd = Cd; f.dc0 = dc0; f.n = n;
     f.B = k.B; f.H = H; f.W = W; f.scale = scale; f.accumulate = accumulate; f.mask = mask;
-    f.add = add; f.dst2 = dst2;
+    f.add = add; f.dst2 = dst2; f.amax = amax;
     hipLaunchKernelGGL(fold_reflect_kernel, g1d((long)k.B * H * W * (n / 4)), dim3(256), 0, k.st, f);
     return hip_ok();
 }
@@ -1057,14 +1035,16 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         if (C % 8 == 0) {                                                               // g_U (ReLU'd)
             hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * 9), dim3(256), 0, st, P.final_w, 1, C, ws.wT);
             hipLaunchKernelGGL(dgrad_final_kernel, g1d(HW * (C / 8)), dim3(256), 0, st, (const float *)ws.gpre,
-                               (const float *)ws.wT, (const float *)sv.u, ws.gU, B, H, W, C);
+                               (const float *)ws.wT, (const float *)sv.u, ws.gU, B, H, W, C, scale_slots(k));
             CHECK(hip_ok());
         } else {
             CHECK(dgrad_vec(k, d, P.final_w));
+            hipLaunchKernelGGL(absmax_publish_kernel, dim3(1024), dim3(256), 0, st, (const float *)ws.gU, (long)HW * C,
+                               scale_slots(k));
         }
         // upsample conv wgrad as a stride-1 wgrad over the materialised up(h) (in dxpF, which
         // the dgrad below overwrites); the gradient scale is shared with that dgrad
-        const float *gsu = grad_scale(k, ws.gU, HW * C);
+        const float *gsu = scale_of(k);
         hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
         CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
@@ -1080,14 +1060,14 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     // ---- 3. ConvLSTM ---------------------------------------------------------------------
     hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
-                       io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C);
-    const float *gsc = grad_scale(k, ws.Gl, hw * 4 * C);
+                       io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C, scale_slots(k));
+    const float *gsc = scale_of(k);
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
     CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y));        // relu(Dg) mask
+    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y, nullptr, nullptr, scale_slots(k)));   // relu(Dg) mask
     if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
-    gsc = grad_scale(k, ws.gy, hw * C);
+    gsc = scale_of(k);
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
     CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr, g.g_z));   // g_z + fold
@@ -1114,18 +1094,18 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         }
         if (1024 % (2 * C) == 0)
             hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, ws.gv, ws.dlp, hw, 2 * C);
+                               lam, ws.gv, ws.dlp, hw, 2 * C, scale_slots(k));
         else
             hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, ws.gv, ws.dlp, hw, 2 * C);
+                               lam, ws.gv, ws.dlp, hw, 2 * C, scale_slots(k));
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
-        gsc = grad_scale(k, ws.gv, hw * 2 * C);
+        gsc = scale_of(k);
         CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b, gsc));
         CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1));   // gx1 += too
+        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));   // gx1 += too
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
-        gsc = grad_scale(k, ws.gxk, hw * C);
+        gsc = scale_of(k);
         CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b, gsc));
         CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, ws.gv));   // identity path + fold
@@ -1138,21 +1118,22 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     hipLaunchKernelGGL(lstc_bwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st, (const float *)sv.gi,
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
-                       ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C);
-    gsc = grad_scale(k, ws.Go, hw * 2 * C);
+                       ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C, scale_slots(k, 0), scale_slots(k, 1));
+    gsc = scale_of(k);                                   // Go; Gl's scale is the next slot set
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
     CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr, nullptr, nullptr,
+               scale_slots(k, 1)));                           // gz0 is final here: its slot set follows Gl's
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
-    gsc = grad_scale(k, ws.Gl, hw * 4 * C);
+    gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
     CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
-    gsc = grad_scale(k, ws.gz0, hw * 2 * C);
+    gsc = scale_of(k);                                   // gz0 (published by its last fold)
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
     CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
@@ -1558,8 +1539,9 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
-    // the gradient-scale slots {amax, ticket} start at zero (absmax_scale_kernel re-zeroes them)
-    if (hipMemsetAsync(k.ws.amax, 0, 8 * sizeof(unsigned), k.st) != hipSuccess) return CISTA_ERR_HIP;
+    // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
+    if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
+        return CISTA_ERR_HIP;
     return run_backward(k, *params, *io, sv, g, *pg);
 }
 }  // extern "C"

@@ -32,6 +32,7 @@ struct FoldArgs {
     const float *mask;     // optional, applied to the result (NHWC, Cd channels)
     const float *add;      // optional (accumulate == 0): dst = add + fold (add laid out as dst)
     float *dst2;           // optional second destination (laid out as dst): dst2 += fold
+    unsigned *amax;        // optional: publish max |dst| (after the mask) to these slots
 };
 
 __device__ __forceinline__ int refl_sources(int i, int n, int (&out)[3]) {
@@ -44,11 +45,36 @@ __device__ __forceinline__ int refl_sources(int i, int n, int (&out)[3]) {
     return k;
 }
 
+// Per-tensor |x| maximum for the power-of-two gradient scales of the split-f16 dgrad / wgrad,
+// accumulated by the kernel that PRODUCES the gradient: a workgroup maximum (every thread of the
+// 256-thread block calls this, with 0 for no element), then one atomicMax of its bits (non-
+// negative floats order as unsigned; fmaxf drops NaN, inf stays inf) into one of 256 slots on
+// separate 64-B lines, so no address sees more than ~1/256 of the workgroups.  slots_scale_kernel
+// turns the slots into {s, 1/s} and re-zeroes them.  (Replaces a separate absmax pass per
+// gradient tensor, 16 us each at B = 8.)
+constexpr int AMAX_SLOTS = 256, AMAX_STRIDE = 16;
+__device__ __forceinline__ void amax_publish(unsigned *slots, float m) {
+    __shared__ float amax_red[4];
+    __syncthreads();                            // a previous call's reads of amax_red are done
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) amax_red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const float b = fmaxf(fmaxf(amax_red[0], amax_red[1]), fmaxf(amax_red[2], amax_red[3]));
+        if (b > 0.0f) atomicMax(slots + (blockIdx.x & (AMAX_SLOTS - 1)) * AMAX_STRIDE, __float_as_uint(b));
+    }
+}
+__device__ __forceinline__ float amax4f(float m, const float4 &v) {
+    return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+
 __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
     const int g4 = a.n / 4;
     const long total = (long)a.B * a.H * a.W * g4;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
+    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx0 < total;
+    if (!a.amax && !live) return;               // (a block that publishes keeps every thread)
+    const long idx = live ? idx0 : total - 1;   // dead threads recompute the last item, store nothing
     const int c = (int)(idx % g4) * 4;
     const long pix = idx / g4;
     const int x = (int)(pix % a.W);
@@ -70,7 +96,7 @@ __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
         const float4 o = a.accumulate ? *d : *(const float4 *)(a.add + od);
         r.x = o.x + f.x; r.y = o.y + f.y; r.z = o.z + f.z; r.w = o.w + f.w;
     }
-    if (a.dst2) {
+    if (a.dst2 && live) {
         float4 *d2 = (float4 *)(a.dst2 + od);
         const float4 o = *d2;
         *d2 = make_float4(o.x + f.x, o.y + f.y, o.z + f.z, o.w + f.w);
@@ -80,7 +106,8 @@ __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
         r.x = m.x > 0.f ? r.x : 0.f; r.y = m.y > 0.f ? r.y : 0.f;
         r.z = m.z > 0.f ? r.z : 0.f; r.w = m.w > 0.f ? r.w : 0.f;
     }
-    *d = r;
+    if (live) *d = r;
+    if (a.amax) amax_publish(a.amax, live ? amax4f(0.0f, r) : 0.0f);
 }
 
 // dgrad weight packing: B fragment of the dgrad conv = W[k=cout][col=cin] at the flipped tap
@@ -647,7 +674,6 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
     float *xmx = reinterpret_cast<float *>(sm + 2 * WT_BUF);     // [4] loader X maxima (rare path)
     int *xfl = reinterpret_cast<int *>(xmx + 4);                 // [2][4] per-buffer overflow flags
-    float *xsc = xmx + 12;                                       // [1] new X pre-scale (rare path)
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ncb = (a.Cin + 63) / 64;
     const int co0 = (blockIdx.x / ncb) * 64, ci0 = (blockIdx.x % ncb) * 64;
@@ -1273,11 +1299,14 @@ __global__ __launch_bounds__(256) void dgrad_vec_kernel(const DgradSmallArgs a, 
 // channels): two float4 weight loads ([9][C] layout, L1-resident) per tap feed 8 FMAs; the
 // general dgrad_vec_kernel spent 4 threads and 64-bit index math per such group (211 us at B=8).
 __global__ __launch_bounds__(256) void dgrad_final_kernel(const float *G, const float *WT, const float *mask,
-                                                          float *dX, int B, int H, int W, int C) {
+                                                          float *dX, int B, int H, int W, int C,
+                                                          unsigned *amax) {
     const int c8 = C >> 3;
     const long total = (long)B * H * W * c8;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= total) return;
+    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx0 < total;
+    if (!amax && !live) return;
+    const long idx = live ? idx0 : total - 1;
     const int c = (int)(idx % c8) * 8;
     const long pix = idx / c8;
     const int plane = H * W;
@@ -1301,8 +1330,11 @@ __global__ __launch_bounds__(256) void dgrad_final_kernel(const float *G, const 
     s0.z = m0.z > 0.0f ? s0.z : 0.0f; s0.w = m0.w > 0.0f ? s0.w : 0.0f;
     s1.x = m1.x > 0.0f ? s1.x : 0.0f; s1.y = m1.y > 0.0f ? s1.y : 0.0f;
     s1.z = m1.z > 0.0f ? s1.z : 0.0f; s1.w = m1.w > 0.0f ? s1.w : 0.0f;
-    *reinterpret_cast<float4 *>(dX + o) = s0;
-    *reinterpret_cast<float4 *>(dX + o + 4) = s1;
+    if (live) {
+        *reinterpret_cast<float4 *>(dX + o) = s0;
+        *reinterpret_cast<float4 *>(dX + o + 4) = s1;
+    }
+    if (amax) amax_publish(amax, live ? amax4f(amax4f(0.0f, s0), s1) : 0.0f);
 }
 
 // W0 (stride 2) dgrad on the zero-padded input domain: dxp (B, H+2, W+2, Cin) gets
@@ -1398,9 +1430,11 @@ __global__ void sigmoid_bwd_kernel(const float *g, const float *y, float *out, l
 // order) and g_c_prev (C; skipped when NULL).
 __global__ void lstm_bwd_kernel(const float *gates, const float *c, const float *c_prev,
                                 const float *gh, const float *gc, float *G, float *gcp, long npix,
-                                int C) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npix * C) return;
+                                int C, unsigned *amax) {
+    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx0 < npix * C;
+    if (!amax && !live) return;
+    const long idx = live ? idx0 : npix * C - 1;
     const long p = idx / C;
     const int ch = (int)(idx % C);
     const float *gt = gates + p * 4 * C;
@@ -1411,11 +1445,16 @@ __global__ void lstm_bwd_kernel(const float *gates, const float *c, const float 
     const float dh = gh ? gh[idx] : 0.0f;
     const float dc = (gc ? gc[idx] : 0.0f) + dh * o * (1.0f - th * th);
     float *Gp = G + p * 4 * C;
-    Gp[ch] = dc * g * i * (1.0f - i);
-    Gp[C + ch] = dc * cp * r * (1.0f - r);
-    Gp[2 * C + ch] = dh * th * o * (1.0f - o);
-    Gp[3 * C + ch] = dc * i * (1.0f - g * g);
-    if (gcp) gcp[idx] = dc * r;
+    const float v0 = dc * g * i * (1.0f - i), v1 = dc * cp * r * (1.0f - r);
+    const float v2 = dh * th * o * (1.0f - o), v3 = dc * i * (1.0f - g * g);
+    if (live) {
+        Gp[ch] = v0;
+        Gp[C + ch] = v1;
+        Gp[2 * C + ch] = v2;
+        Gp[3 * C + ch] = v3;
+        if (gcp) gcp[idx] = dc * r;
+    }
+    if (amax) amax_publish(amax, live ? amax4f(0.0f, make_float4(v0, v1, v2, v3)) : 0.0f);
 }
 
 // softshrink backward (reference base_layers.py:11-12): z = relu(v-l) - relu(-v-l)
@@ -1424,8 +1463,10 @@ __global__ void lstm_bwd_kernel(const float *gates, const float *c, const float 
 // thread; requires 256 % C == 0), coalesced over channels.
 __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, const float *v,
                                                              const float *lam, float *gv,
-                                                             float *dl_partial, long npix, int C) {
+                                                             float *dl_partial, long npix, int C,
+                                                             unsigned *amax) {
     __shared__ float red[256];
+    float mx = 0.0f;
     const int c = threadIdx.x % C;
     const float l = lam[c];
     const long total = npix * C;
@@ -1434,6 +1475,7 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
         const float vv = v[i], g = gz[i];
         const bool up = vv > l, dn = vv < -l;
         gv[i] = g * ((up ? 1.0f : 0.0f) + (dn ? 1.0f : 0.0f));
+        mx = fmaxf(mx, fabsf(gv[i]));
         acc += g * ((dn ? 1.0f : 0.0f) - (up ? 1.0f : 0.0f));
     }
     red[threadIdx.x] = acc;
@@ -1443,14 +1485,17 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
         for (int k = threadIdx.x; k < 256; k += C) s += red[k];
         dl_partial[(size_t)blockIdx.x * C + threadIdx.x] = s;
     }
+    if (amax) amax_publish(amax, mx);
 }
 
 // softshrink_bwd_kernel over float4 channel groups (1024 % C == 0): the same gv and, per
 // workgroup, the same dlambda partials up to the order of the per-channel sums
 __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, const float *v,
                                                               const float *lam, float *gv,
-                                                              float *dl_partial, long npix, int C) {
+                                                              float *dl_partial, long npix, int C,
+                                                              unsigned *amax) {
     __shared__ float4 red[256];
+    float mx = 0.0f;
     const int cq = C >> 2, c = (threadIdx.x % cq) * 4;
     const float4 l = *reinterpret_cast<const float4 *>(lam + c);
     const long total = npix * cq;
@@ -1470,6 +1515,7 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
         r.z = one(vv.z, g.z, l.z, acc.z);
         r.w = one(vv.w, g.w, l.w, acc.w);
         o4[i] = r;
+        mx = amax4f(mx, r);
     }
     red[threadIdx.x] = acc;
     __syncthreads();
@@ -1480,6 +1526,7 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
         }
         *reinterpret_cast<float4 *>(dl_partial + (size_t)blockIdx.x * C + 4 * threadIdx.x) = s;
     }
+    if (amax) amax_publish(amax, mx);
 }
 
 // z = softshrink(v, lambda) over float4 channel groups (C % 4 == 0)
@@ -1525,9 +1572,12 @@ __global__ void softshrink_fwd_kernel(const float *v, const float *lam, float *z
 // gcp (Cz, nullable).
 __global__ void lstc_bwd_kernel(const float *gi_, const float *gf_, const float *go_, const float *z0,
                                 const float *c, const float *c_prev, const float *gz, const float *gcl,
-                                float *Gg, float *Go, float *gz0, float *gcp, long npix, int Cz) {
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (idx >= npix * Cz) return;
+                                float *Gg, float *Go, float *gz0, float *gcp, long npix, int Cz,
+                                unsigned *amax_go, unsigned *amax_gg) {
+    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx0 < npix * Cz;
+    if (!amax_go && !live) return;
+    const long idx = live ? idx0 : npix * Cz - 1;
     const long p = idx / Cz;
     const int ch = (int)(idx % Cz);
     const float i = gi_[idx], f = gf_[idx], o = go_[idx];
@@ -1535,11 +1585,19 @@ __global__ void lstc_bwd_kernel(const float *gi_, const float *gf_, const float 
     const float cp = c_prev ? c_prev[idx] : 0.0f;
     const float dz = gz[idx];
     const float dc = (gcl ? gcl[idx] : 0.0f) + dz * o * (1.0f - th * th);
-    Go[idx] = dz * th * o * (1.0f - o);
-    Gg[p * 2 * Cz + ch] = dc * z0[idx] * i * (1.0f - i);
-    Gg[p * 2 * Cz + Cz + ch] = dc * cp * f * (1.0f - f);
-    gz0[idx] = dc * i;
-    if (gcp) gcp[idx] = dc * f;
+    const float vo = dz * th * o * (1.0f - o);
+    const float vi = dc * z0[idx] * i * (1.0f - i), vf = dc * cp * f * (1.0f - f);
+    if (live) {
+        Go[idx] = vo;
+        Gg[p * 2 * Cz + ch] = vi;
+        Gg[p * 2 * Cz + Cz + ch] = vf;
+        gz0[idx] = dc * i;
+        if (gcp) gcp[idx] = dc * f;
+    }
+    if (amax_go) {                              // both or neither (the host passes both)
+        amax_publish(amax_go, live ? fabsf(vo) : 0.0f);
+        amax_publish(amax_gg, live ? fmaxf(fabsf(vi), fabsf(vf)) : 0.0f);
+    }
 }
 
 // bilinear x2 (align_corners=False) backward: gh[b,y,x,c] (+)= sum over up-pixels (Y, X) of
