@@ -762,9 +762,12 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.dxp = take((size_t)B * (h + 2) * (w + 2) * 4 * C);
     s.gy = take(hw * C);
     s.gz = take(hw * 2 * C);
-    s.gv = take(hw * 2 * C);
-    s.gxk = take(hw * C);
-    s.zk = take(hw * 2 * C);
+    // the ISTA iterations' gradients and iterates, stacked [iteration][B][h][w][C] so that the
+    // tied D / P weight gradients are one wgrad launch each over all iterations
+    const size_t nd = cfg.depth > 0 ? (size_t)cfg.depth : 1;
+    s.gv = take(nd * hw * 2 * C);
+    s.gxk = take(nd * hw * C);
+    s.zk = take(nd * hw * 2 * C);
     s.gx1 = take(hw * C);
     s.Go = take(hw * 2 * C);
     s.gz0 = take(hw * 2 * C);
@@ -773,7 +776,7 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.dlp = take((size_t)2 * C * 512);
     s.wT = take((size_t)9 * C * C);
     s.amax = reinterpret_cast<unsigned *>(take((size_t)8 * AMAX_SLOTS * AMAX_STRIDE));
-    s.scl = take(32);
+    s.scl = take(32 + 4 * nd + 4);   // 8 rotating pairs, the ISTA P / D pairs per iteration, their minima
     s.bytes = off;
     return s;
 }
@@ -822,22 +825,30 @@ int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP
 unsigned *scale_slots(Bwd &k, int ahead = 0) {
     return k.ws.amax + (size_t)((k.slot + ahead) & 7) * AMAX_SLOTS * AMAX_STRIDE;
 }
+// the smallest of n scale pairs (the largest gradient of a stacked wgrad) -> out
+__global__ void min_scale_kernel(const float *pairs, int n, float *out) {
+    if (threadIdx.x != 0) return;
+    int j = 0;
+    for (int i = 1; i < n; ++i) j = pairs[2 * i] < pairs[2 * j] ? i : j;
+    out[0] = pairs[2 * j];
+    out[1] = pairs[2 * j + 1];
+}
 // a gradient whose producer does not publish: one grid-stride |max| pass into the slots
 __global__ __launch_bounds__(256) void absmax_publish_kernel(const float *x, long n, unsigned *slots) {
     float m = 0.0f;
     for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) m = fmaxf(m, fabsf(x[i]));
     amax_publish(slots, m);
 }
-const float *scale_of(Bwd &k);
+const float *scale_of(Bwd &k, float *dst = nullptr);
 const float *grad_scale(Bwd &k, const float *G, long n) {
     const long blocks = (n + 255) / 256;
     hipLaunchKernelGGL(absmax_publish_kernel, dim3((unsigned)(blocks < 1 ? 1 : blocks > 1024 ? 1024 : blocks)), dim3(256),
                        0, k.st, G, n, scale_slots(k));
     return scale_of(k);
 }
-const float *scale_of(Bwd &k) {
+const float *scale_of(Bwd &k, float *dst) {
     unsigned *sl = scale_slots(k);
-    float *sc = k.ws.scl + 2 * (k.slot & 7);
+    float *sc = dst ? dst : k.ws.scl + 2 * (k.slot & 7);
     ++k.slot;
     hipLaunchKernelGGL(slots_scale_kernel, dim3(1), dim3(AMAX_SLOTS), 0, k.st, sl, sc);
     return hipGetLastError() == hipSuccess ? sc : nullptr;
@@ -864,12 +875,13 @@ constexpr int NCU = 256;      // MI355X compute units (8 XCDs x 32)
 template <int XS>
 int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, int x0c,
           const float *X1, int x1c, int Cin, int Hin, int Win, int Hout, int Wout, float *dst,
-          float sign, int accumulate, float *db, const float *gsc = nullptr) {
+          float sign, int accumulate, float *db, const float *gsc = nullptr, int Bn = 0) {
     WgradArgs a;
     memset(&a, 0, sizeof(a));
     a.G = G; a.Gc = Gc; a.Goff = Goff;
     a.X0 = X0; a.x0c = x0c; a.X1 = X1; a.x1c = x1c;
-    a.B = k.B; a.Hin = Hin; a.Win = Win; a.Hout = Hout; a.Wout = Wout;
+    a.B = Bn > 0 ? Bn : k.B;                 // Bn: samples of a stacked (iterations x batch) G / X
+    a.Hin = Hin; a.Win = Win; a.Hout = Hout; a.Wout = Wout;
     a.Cout = Cout; a.Cin = Cin;
     a.partial = k.ws.part;
     a.bpartial = db ? k.ws.bpart : nullptr;
@@ -879,7 +891,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.TH = WS_TH; a.TW = WS_TW;
         a.tiles_y = (Hout + WS_TH - 1) / WS_TH;
         a.tiles_x = (Wout + WS_TW - 1) / WS_TW;
-        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        const int ntiles = a.B * a.tiles_y * a.tiles_x;
         if (CISTA_WGRAD_TR) {
             // 64 x 64 blocks, one 8-wave workgroup per CU: splits fill the CUs once (and fit
             // the partial buffer: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9)
@@ -912,7 +924,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.TH = 16; a.TW = 16;                                // We / Wi: VALU over NCHW planes
         a.tiles_y = (Hout + 15) / 16;
         a.tiles_x = (Wout + 15) / 16;
-        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        const int ntiles = a.B * a.tiles_y * a.tiles_x;
         const int ns = ntiles < 512 ? ntiles : 512;
         a.nsplit = ns;
         switch (Cin) {
@@ -931,7 +943,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.tiles_y = (Hout + 15) / 16;
         a.tiles_x = (Wout + 15) / 16;
         const int ncb = Cin / 32;
-        const int ntiles = k.B * a.tiles_y * a.tiles_x;
+        const int ntiles = a.B * a.tiles_y * a.tiles_x;
         int ns = 512 / ncb;
         ns = ns > ntiles ? ntiles : ns;
         ns = ns < 1 ? 1 : ns;
@@ -948,7 +960,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     a.tiles_x = (Wout + a.TW - 1) / a.TW;
     a.Cout = Cout; a.Cin = Cin;
     const int nblk = ((Cout + 31) / 32) * ((Cin + 31) / 32);
-    const int ntiles = k.B * a.tiles_y * a.tiles_x;
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
     int ns = WG_BLOCKS / nblk;
     ns = ns > ntiles ? ntiles : ns;
     ns = ns < 1 ? 1 : ns;
@@ -1083,35 +1095,45 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     if (hipMemsetAsync(ws.gx1, 0, (size_t)hw * C * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     const int nbl = 512;   // softshrink_bwd blocks (lambda partials [nbl][2C])
+    float *sclP = ws.scl + 32, *sclD = sclP + 2 * D;      // per-iteration scale pairs of gv / gxk
     for (int it = D - 1; it >= 0; --it) {
         const float *v = sv.v + (size_t)it * hw * 2 * C;
-        const float *xk = sv.xs + (size_t)it * hw * C;
-        const float *zk = sv.zl;
-        if (it > 0) {
+        float *gv = ws.gv + (size_t)it * hw * 2 * C, *gxk = ws.gxk + (size_t)it * hw * C;
+        float *zk = ws.zk + (size_t)it * hw * 2 * C;      // D's input of this iteration (its wgrad X)
+        if (it > 0)
             hipLaunchKernelGGL(softshrink_fwd4_kernel, g1d(hw * 2 * C / 4), dim3(256), 0, st,
-                               sv.v + (size_t)(it - 1) * hw * 2 * C, lam, ws.zk, hw, 2 * C);
-            zk = ws.zk;
-        }
+                               sv.v + (size_t)(it - 1) * hw * 2 * C, lam, zk, hw, 2 * C);
+        else if (hipMemcpyAsync(zk, sv.zl, (size_t)hw * 2 * C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return CISTA_ERR_HIP;
         if (1024 % (2 * C) == 0)
             hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, ws.gv, ws.dlp, hw, 2 * C, scale_slots(k));
+                               lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
         else
             hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, ws.gv, ws.dlp, hw, 2 * C, scale_slots(k));
+                               lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
-        gsc = scale_of(k);
-        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, xk, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, it != D - 1, pg.P_b, gsc));
-        CHECK(dgrad_conv(k, CV_P, ws.gv, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, C, 0, ws.gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));   // gx1 += too
+        gsc = scale_of(k, sclP + 2 * it);
+        CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, C, 0, gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));   // gx1 += too
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
-        gsc = scale_of(k);
-        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, it != D - 1, pg.D_b, gsc));
-        CHECK(dgrad_conv(k, CV_D, ws.gxk, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, ws.gv));   // identity path + fold
+        gsc = scale_of(k, sclD + 2 * it);
+        CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, gv));   // identity path + fold
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
         hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
                            pg.lambda, it != D - 1);
+    }
+    if (D > 0) {
+        // tied D / P weights: one wgrad over all iterations each (G and X stacked as D x B samples),
+        // the split scale the smallest of the iterations' (their largest gradient)
+        float *sP = sclD + 2 * D, *sD = sP + 2;
+        hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclP, D, sP);
+        hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclD, D, sD);
+        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0, pg.P_b, sP,
+                           D * B));
+        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, ws.zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
+                           D * B));
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------
     // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part)
