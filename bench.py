@@ -292,10 +292,10 @@ def train_main(args, torch, vd, rank, world, device):
     # (SURVEY 8(d) "training FLOPs ~ 3x fwd"), run on the same split-f16 MFMA peak
     train_tf = frames / elapsed / world * 3 * 2 * macs_frame / 1e12
     peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
-    roofline = dict(bound="mfma", achieved=round(train_tf, 2), peak=round(peak, 1), unit="TFLOP/s",
-                    frac=round(train_tf / peak, 4), traffic=None, kernel="whole BPTT step (per GPU)",
-                    note="achieved = 3 x forward algorithmic FLOPs per frame x frames/s per GPU; "
-                         "peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+    roofline = train_roofline(torch, model, _lib, B, H, W, device)
+    roofline["step_tflops_est"] = round(train_tf, 2)
+    roofline["step_frac_est"] = round(train_tf / peak, 4)
+    roofline["step_note"] = "whole BPTT step: 3 x forward algorithmic FLOPs per frame x frames/s per GPU"
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = train_cpu_baseline(torch, model, vox, target, L, H, W)
@@ -315,6 +315,69 @@ def train_main(args, torch, vd, rank, world, device):
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}), flush=True)
     if world > 1:
         torch.distributed.destroy_process_group()
+
+
+def train_roofline(torch, model, lib_mod, B, H, W, device, reps=10):
+    """The training step's dominant kernel: the tied ISTA P weight gradient over all depth
+    iterations (split-f16 wgrad_tr_kernel + its partial reduction, cista_wgrad_ista_p), timed
+    alone with HIP events on the stream it is launched on, at the bench's shapes (synthetic G / X
+    of the same sizes; the work does not depend on the values).  Algorithmic FLOPs per launch =
+    2 x 9 x 2C x C x (depth x B x h x w); HBM bytes per launch from the committed PMC passes of
+    this build (profiles/rNN_train_pmc_traffic.json, scripts/pmc_train_wgrad.sh)."""
+    L = lib_mod.lib()
+    C, D = model.base_channels, model.depth
+    h, w = H // 2, W // 2
+    n = D * B * h * w
+    g = torch.Generator(device=device).manual_seed(11)
+    G = (torch.rand(n * 2 * C, device=device, generator=g) * 2 - 1) * 8192.0    # split scale folded in
+    X = torch.rand(n * C, device=device, generator=g) * 2 - 1
+    sc = torch.tensor([1.0, 1.0], device=device)
+    dW = torch.empty(2 * C * C * 9, device=device)
+    db = torch.empty(2 * C, device=device)
+    ws = model.train_workspace(B, H, W, device)
+    cfg = model._cfg()
+    stream = torch.cuda.current_stream(device)
+    args = (ctypes.byref(cfg), B, H, W, G.data_ptr(), X.data_ptr(), sc.data_ptr(), dW.data_ptr(), db.data_ptr(),
+            ws.data_ptr(), ws.numel(), stream.cuda_stream)
+    for _ in range(2):
+        lib_mod.check(L.cista_wgrad_ista_p(*args), "cista_wgrad_ista_p")
+    e0 = torch.cuda.Event(enable_timing=True)
+    e1 = torch.cuda.Event(enable_timing=True)
+    e0.record(stream)
+    for _ in range(reps):
+        L.cista_wgrad_ista_p(*args)
+    e1.record(stream)
+    e1.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    flop = 2.0 * 9 * 2 * C * C * n
+    tf = flop / (ms * 1e-3) / 1e12
+    peak = PEAK_F16_MFMA_TFLOPS / SPLIT_PASSES
+    alg = 4.0 * n * 3 * C                     # G (2C) and X (C) read once, fp32
+    roof = dict(bound="mfma", achieved=round(tf, 2), peak=round(peak, 1), unit="TFLOP/s",
+                frac=round(tf / peak, 4), traffic=None,
+                kernel="ista_P_wgrad (wgrad_tr_kernel + reduce_partials_kernel, all %d iterations)" % D,
+                launch_ms=round(ms, 4), flop_per_launch=flop, algorithmic_bytes_per_launch=alg,
+                note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean duration "
+                     "(HIP events); peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
+    import glob
+    import hashlib
+    tfiles = sorted(f for f in glob.glob(os.path.join(ROOT, "profiles", "r*_train_pmc_traffic.json"))
+                    if re.fullmatch(r"r\d\d_train_pmc_traffic\.json", os.path.basename(f)))
+    if tfiles:
+        try:
+            tj = json.load(open(tfiles[-1]))
+            roof["traffic_source"] = os.path.relpath(tfiles[-1], ROOT)
+            tl = tj["layers"].get("ista_P_wgrad")
+            if tl and tj.get("lib_sha256") == hashlib.sha256(open(lib_mod.LIB_PATH, "rb").read()).hexdigest():
+                roof["traffic"] = tl["hbm_bytes_per_launch"]
+                gbps = tl["hbm_bytes_per_launch"] / (ms * 1e-3) / 1e9
+                roof["hbm_achieved_GBps"] = round(gbps, 1)
+                roof["hbm_frac"] = round(gbps / (HBM_TBPS * 1e3), 4)
+            else:
+                roof["traffic_note"] = "no PMC traffic of this build in " + roof["traffic_source"]
+        except (OSError, ValueError, KeyError):
+            pass
+    return roof
 
 
 def train_cpu_baseline(torch, model, vox, target, L, H, W, min_s=10.0, max_steps=4):

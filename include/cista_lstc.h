@@ -229,6 +229,15 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
                    const cista_param_grads *pgrads, void *workspace, size_t workspace_bytes,
                    void *stream);
 
+/* Timing / PMC hook (bench.py --mode train): the backward's dominant launch on its own -- the
+ * tied ISTA P weight gradient over all `depth` iterations (split-f16 wgrad + partial reduction),
+ * as cista_backward runs it.  G (depth*B, h, w, 2C) and X (depth*B, h, w, C) NHWC fp32, gscale
+ * {s, 1/s} the power-of-two fp16 split scale of G (device), dW (2C, C, 3, 3) and db (2C) written.
+ * workspace: cista_train_workspace_bytes. */
+int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float *G, const float *X,
+                       const float *gscale, float *dW, float *db, void *workspace,
+                       size_t workspace_bytes, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -99,6 +99,8 @@ def _declare(lib):
         "cista_backward": (c_int, [P(CistaConfig), c_void_p, P(CistaParams), c_int, c_int, c_int,
                                    P(CistaFrameIO), c_void_p, c_size_t, P(CistaGradIO), c_size_t,
                                    P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
+        "cista_wgrad_ista_p": (c_int, [P(CistaConfig), c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                       c_void_p, c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
         "cista_sequence_capture": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO), c_int,

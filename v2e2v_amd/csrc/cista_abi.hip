@@ -268,14 +268,17 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #ifndef CISTA_SMALL_GRID
 #define CISTA_SMALL_GRID 1   // latency tiles for grids that would not fill the chip (small B)
 #endif
+#ifndef CISTA_DGRAD_SMALL
+#define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
+#endif
 #ifndef CISTA_WIDE
 #define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
 #endif
 // fewer than ~1.5 workgroups per CU with the throughput configuration (px x cols per WG)
-inline bool small_grid(const ConvArgs &a, int wg_px, int wg_cols) {
+inline bool small_grid(const ConvArgs &a, int wg_px, int wg_cols, int limit = 384) {
 #if CISTA_SMALL_GRID
     const long px = (long)a.B * a.Hout * a.Wout;
-    return ((px + wg_px - 1) / wg_px) * ((a.N + wg_cols - 1) / wg_cols) < 384;
+    return ((px + wg_px - 1) / wg_px) * ((a.N + wg_cols - 1) / wg_cols) < limit;
 #else
     (void)a; (void)wg_px; (void)wg_cols;
     return false;
@@ -306,6 +309,12 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
     } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_S2D)) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
         constexpr bool FWD = STAGE == STAGE_S1 || STAGE == STAGE_S2D;
+        if constexpr (STAGE == STAGE_ZP2 && G == 1) {
+            // training dgrads at small batches (B = 8): below ~4 throughput workgroups per CU
+            // the launch is one workgroup lifetime long; 64 x 64 workgroups give 4x as many
+            if (a.N % 64 == 0 && small_grid(a, 192, a.N % 128 == 0 ? 128 : 64, CISTA_DGRAD_SMALL))
+                return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
+        }
         if constexpr (FWD) {
             // small batches (B = 1 is the reference harness's case): the throughput tiles below
             // leave most CUs idle, so 64-pixel x 64-column workgroups trade MFMA efficiency
@@ -1505,6 +1514,26 @@ size_t cista_train_workspace_bytes(const cista_config *cfg, int B, int H, int W)
 
 static int train_supported(const cista_config *cfg) {
     return (cfg->base_channels == 64 || cfg->base_channels == 32) ? CISTA_OK : CISTA_ERR_UNSUPPORTED;
+}
+
+// the backward's dominant launch on its own (timing / PMC hook): the tied ISTA P weight
+// gradient over all depth iterations, exactly as run_backward launches it
+int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float *G, const float *X,
+                       const float *gscale, float *dW, float *db, void *workspace, size_t workspace_bytes,
+                       void *stream) {
+    if (!cfg_ok(cfg) || train_supported(cfg) != CISTA_OK || cfg->depth < 1) return CISTA_ERR_UNSUPPORTED;
+    if (!G || !X || !gscale || !dW || !db || !workspace || B <= 0) return CISTA_ERR_INVALID;
+    if ((H & 1) || (W & 1) || H < 4 || W < 4) return CISTA_ERR_INVALID;
+    Bwd k;
+    k.cfg = cfg; k.packed = nullptr; k.L = make_layout(*cfg);
+    k.B = B; k.H = H; k.W = W; k.h = H / 2; k.w = W / 2; k.C = cfg->base_channels;
+    k.st = static_cast<hipStream_t>(stream);
+    k.ws = carve_bwd(workspace, *cfg, B, H, W);
+    k.slot = 0;
+    if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
+    const int C = k.C;
+    return wgrad<XS_S1>(k, G, 2 * C, 0, 2 * C, X, C, nullptr, 0, C, k.h, k.w, k.h, k.w, dW, 1.0f, 0, db, gscale,
+                        cfg->depth * B);
 }
 
 int cista_forward_train(const cista_config *cfg, const void *packed, int B, int H, int W,
