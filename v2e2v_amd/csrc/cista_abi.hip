@@ -210,7 +210,10 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
     constexpr bool SEG = STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_CLAMP || STAGE == STAGE_S2D;
-    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * 256 : 0, NI ? 2 : 1, OCC, SEG);
+    constexpr int NWV = WM * WN, NT = NWV * 64;     // waves, threads per workgroup
+    // OCC = waves per SIMD the register budget is sized for (__launch_bounds__): OCC * 4 / NWV
+    // workgroups share a CU's LDS
+    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG);
     if (a.border == 1)          // rows 0 and Hout-1 in 1-row tiles
         t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S), 0};
     else if (a.border == 2)     // columns 0 and Wout-1 in 1-column tiles
@@ -239,12 +242,12 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // and the double-buffered staging reads inputs with 32-bit element offsets
     if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 ? 4 : 1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
     if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
-    const size_t epi_lds = (size_t)4 * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
-    // + 8 words of range-pass scratch right after the epilogue's LDS (inside the dead staging
-    // images when those are larger)
+    const size_t epi_lds = (size_t)NWV * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
+    // + 2 x NWV words of range-pass scratch right after the epilogue's LDS (inside the dead
+    // staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    const size_t lds = t.lds > epi_lds + 32 ? t.lds : epi_lds + 32;
-    hipLaunchKernelGGL(kern, grid, dim3(256), lds, st, a);
+    const size_t lds = t.lds > epi_lds + 8 * NWV ? t.lds : epi_lds + 8 * NWV;
+    hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
 
@@ -267,6 +270,9 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #endif
 #ifndef CISTA_SMALL_GRID
 #define CISTA_SMALL_GRID 1   // latency tiles for grids that would not fill the chip (small B)
+#endif
+#ifndef CISTA_ISTA8
+#define CISTA_ISTA8 0            // 1: ISTA D conv on 8-wave workgroups (measured 5 % slower), 2: also ISTA P (spills)
 #endif
 #ifndef CISTA_DGRAD_SMALL
 #define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
@@ -324,6 +330,12 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
                 if constexpr (G == 4) return launch_conv_cfg<1, 4, 4, 1, STAGE, EPI, G, true, 2>(a, st);
                 else return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
             }
+        }
+        if constexpr (CISTA_ISTA8 && STAGE == STAGE_S1 && G == 1 && (EPI == EPI_ISTA_D || EPI == EPI_ISTA_P)) {
+            // 8-wave workgroups on the same 192-pixel tiles: 4 waves per SIMD at 2 workgroups
+            // per CU, so one workgroup's staging / epilogue HBM phases overlap more MFMA waves
+            if (a.N == 128 && CISTA_ISTA8 > 1) return launch_conv_cfg<6, 2, 2, 4, STAGE, EPI, G, true, 2, 4>(a, st);
+            if (a.N == 64) return launch_conv_cfg<3, 2, 4, 2, STAGE, EPI, G, true, 2, 4>(a, st);
         }
         if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
             if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);

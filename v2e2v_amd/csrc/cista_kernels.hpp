@@ -306,19 +306,19 @@ __device__ __forceinline__ void stage_load(const ConvArgs &a, int b, int iy0, in
     }
 }
 
-template <int STAGE>
+template <int STAGE, int NT = 256>
 __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int b, int iy0,
                                             int ix0, int HH, int HWd, int HPpad,
                                             const float *seg, int segC, int choff, f16x2 &amax) {
     constexpr int BATCH = STAGE == STAGE_UP ? 2 : 4;
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
-    for (int it0 = threadIdx.x; it0 < nitems; it0 += BATCH * 256) {
+    for (int it0 = threadIdx.x; it0 < nitems; it0 += BATCH * NT) {
         float4 v0[BATCH], v1[BATCH];
         int hps[BATCH], gs[BATCH];
 #pragma unroll
         for (int u = 0; u < BATCH; ++u) {
-            const int it = it0 + u * 256;
+            const int it = it0 + u * NT;
             int hp = ((it >> 5) << 3) | (it & 7);
             gs[u] = (it >> 3) & 3;
             hps[u] = (it < nitems && hp < HP) ? hp : -1;
@@ -339,7 +339,7 @@ __device__ __forceinline__ void stage_chunk(const ConvArgs &a, u32x4 *smem, int 
 // Split staging for the double-buffered K loop: issue the global loads of the NEXT chunk into
 // registers before the current chunk's MFMAs, convert + write them to the other LDS buffer
 // after.  The host guarantees (HP rounded to 8) * 4 <= NI * blockDim.x items.
-template <int STAGE, int NI>
+template <int STAGE, int NI, int NT = 256>
 __device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, int ix0, int HH,
                                             int HWd, const float *seg, int segC, int choff,
                                             float4 (&v0)[NI], float4 (&v1)[NI], int (&hps)[NI],
@@ -348,7 +348,7 @@ __device__ __forceinline__ void stage_issue(const ConvArgs &a, int b, int iy0, i
     const int nitems = ((HP + 7) & ~7) * 4;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-        const int it = threadIdx.x + u * 256;
+        const int it = threadIdx.x + u * NT;
         int hp = ((it >> 5) << 3) | (it & 7);
         gs[u] = (it >> 3) & 3;
         hps[u] = (it < nitems && hp < HP) ? hp : -1;
@@ -379,13 +379,13 @@ __device__ __forceinline__ float absmax8(const float4 &a, const float4 &b) {
     return fmaxf(m0, m1);
 }
 
-template <int STAGE>
+template <int STAGE, int NT = 256>
 __device__ float stage_absmax(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd, const float *seg,
                               int segC, int choff) {
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
     float mx = 0.0f;
-    for (int it = threadIdx.x; it < nitems; it += 256) {
+    for (int it = threadIdx.x; it < nitems; it += NT) {
         const int hp = ((it >> 5) << 3) | (it & 7);
         if (hp >= HP) continue;
         float4 v0, v1;
@@ -399,14 +399,14 @@ __device__ float stage_absmax(const ConvArgs &a, int b, int iy0, int ix0, int HH
 // their source pixel (reflect / zero padding resolved) is computed once per tile; a chunk's
 // load address is then seg + pixel * segC + choff + 8 g in 32-bit arithmetic.
 // spix: pixel index (b, iy, ix) >= 0, -1 = no item, -2 = zero padding (STAGE_ZP2).
-template <int STAGE, int NI>
+template <int STAGE, int NI, int NT = 256>
 __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd,
                                              int (&spix)[NI], int (&hps)[NI], int (&gs)[NI]) {
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-        const int it = threadIdx.x + u * 256;
+        const int it = threadIdx.x + u * NT;
         const int hp = ((it >> 5) << 3) | (it & 7);
         gs[u] = (it >> 3) & 3;
         hps[u] = (it < nitems && hp < HP) ? hp : -1;
@@ -551,7 +551,7 @@ __device__ __forceinline__ void rare_item(const ConvArgs &a, int b, int iy0, int
     }
 }
 
-template <int MT_W, int WM, int NW, int STAGE>
+template <int MT_W, int WM, int NW, int STAGE, int NWV = 4>
 __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32x4 (&acc)[MT_W][NW], int b, int oy0,
                                              int ox0, int wm, int nt0, int nchunks, int kc0) {
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
@@ -572,7 +572,7 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
     for (int kc = 0; kc < nchunks; ++kc) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
-        for (int it = threadIdx.x; it < nitems; it += 256) {
+        for (int it = threadIdx.x; it < nitems; it += NWV * 64) {
             const int hp = ((it >> 5) << 3) | (it & 7);
             if (hp >= HP) continue;
             float4 v0, v1;
@@ -581,10 +581,12 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
         }
     }
     for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
-    float *flm = reinterpret_cast<float *>(smem) + a.lds_flag + 4;
+    float *flm = reinterpret_cast<float *>(smem) + a.lds_flag + NWV;
     if (lane == 0) flm[wave] = mx;
     __syncthreads();
-    mx = fmaxf(fmaxf(flm[0], flm[1]), fmaxf(flm[2], flm[3]));
+    mx = flm[0];
+#pragma unroll
+    for (int w = 1; w < NWV; ++w) mx = fmaxf(mx, flm[w]);
     if (!(mx < 3.0e38f)) return 1.0f;                   // an inf input: the reference gives inf / NaN too
     int e = (int)floorf(log2f(16384.0f / mx));
     e = e < -126 ? -126 : (e > 0 ? 0 : e);
@@ -598,7 +600,7 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
         __syncthreads();                                // the maxima / previous chunk's reads are done
-        for (int it = threadIdx.x; it < nitems; it += 256) {
+        for (int it = threadIdx.x; it < nitems; it += NWV * 64) {
             const int hp = ((it >> 5) << 3) | (it & 7), g = (it >> 3) & 3;
             if (hp >= HP) continue;
             float4 v0, v1;
@@ -647,9 +649,10 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
 // OCC: workgroups per CU the register budget is sized for (LDS: the host's tile choice)
 template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false,
           int OCC = 2>
-__global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
+__global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvArgs a) {
     // NI > 0: double-buffered K loop (two LDS images, next chunk's loads in NI x 8 VGPRs)
-    static_assert(WM * WN == 4, "4 waves per workgroup");
+    constexpr int NWV = WM * WN, NTH = NWV * 64;           // waves, threads
+    static_assert(NWV == 4 || NWV == 8, "4 or 8 waves per workgroup");
     static_assert(NW % G == 0, "a wave must hold whole gate groups");
     extern __shared__ u32x4 smem[];
 
@@ -754,12 +757,12 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         static_assert(PF, "the double-buffered loop uses the prefetching tap schedule");
         // B prefetch depth: deep where the accumulators leave room (the 6 x 2-tile waves)
         constexpr int BPF_MAX = 96 / (NW * 8) - 1;          // ring <= 96 VGPRs
-        constexpr int BPF = MT_W * NW * 4 > 48 ? 1 : (CISTA_BPF < BPF_MAX ? CISTA_BPF : BPF_MAX);
+        constexpr int BPF = (MT_W * NW * 4 > 48 || NWV == 8) ? 1 : (CISTA_BPF < BPF_MAX ? CISTA_BPF : BPF_MAX);
         static_assert(STAGE == STAGE_S1 || STAGE == STAGE_S2 || STAGE == STAGE_ZP2 || STAGE == STAGE_CLAMP ||
                           STAGE == STAGE_S2D,
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
-        stage_pixels<STAGE, NI>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
+        stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
         {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
@@ -822,7 +825,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
         __syncthreads();
-        stage_chunk<STAGE>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff, amax);
+        stage_chunk<STAGE, NTH>(a, smem, b, iy0, ix0, HH, HWd, HPpad, seg, segC, choff, amax);
         __syncthreads();
 
         const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
@@ -876,15 +879,18 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
 
     CISTA_STAMP(11, __builtin_amdgcn_s_memtime());
     if constexpr (CISTA_RANGE_CHECK) {
-        int *fl = reinterpret_cast<int *>(smem) + a.lds_flag;   // [0, 4): per-wave overflow bits
+        int *fl = reinterpret_cast<int *>(smem) + a.lds_flag;   // [0, NWV): per-wave overflow bits
         {
             const _Float16 hm = amax[0] > amax[1] ? amax[0] : amax[1];
             const bool wany = __ballot(__builtin_isinf((float)hm) ? 1 : 0) != 0;
             if (lane == 0) fl[wave] = wany ? 1 : 0;
         }
         __syncthreads();
-        if (CISTA_RERUN && !a.ascale && (fl[0] | fl[1] | fl[2] | fl[3]) != 0)
-            insc = range_rerun<MT_W, WM, NW, STAGE>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0);
+        int anyfl = fl[0];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) anyfl |= fl[w];
+        if (CISTA_RERUN && !a.ascale && anyfl != 0)
+            insc = range_rerun<MT_W, WM, NW, STAGE, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0);
     }
 
     // ---------------------------------- epilogue ----------------------------------------
@@ -923,7 +929,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
         // waiting behind the stores before it (vmcnt is in order)
         __syncthreads();                                   // the last chunk's A reads are done
         float *wfs = reinterpret_cast<float *>(smem);
-        for (int i = threadIdx.x; i < 9 * a.Cout; i += 256) wfs[i] = a.aux0[i];
+        for (int i = threadIdx.x; i < 9 * a.Cout; i += NTH) wfs[i] = a.aux0[i];
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < MT_W; ++m) {
@@ -987,8 +993,8 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
     // per-pixel element offset (pixel * Cout) of the output tensors, -1 outside the image:
     // the items below then need no division, no 64-bit math and no bounds arithmetic
-    int *ptab = reinterpret_cast<int *>(smem) + 4 * 16 * LDT;
-    for (int p = threadIdx.x; p < NPXB; p += 256) {
+    int *ptab = reinterpret_cast<int *>(smem) + NWV * 16 * LDT;
+    for (int p = threadIdx.x; p < NPXB; p += NTH) {
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
@@ -1036,7 +1042,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     // m-tile's worth after each m-tile is consumed): under load an HBM read takes ~5 us, so a
     // one-ahead prefetch made the epilogue a chain of MT_W round trips (scripts/stamps.py)
     constexpr int AUXV = NIT * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
-    constexpr int PD0 = AUXV ? CISTA_AUX_VGPRS / AUXV : MT_W;
+    constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / AUXV : MT_W;   // 8 waves: 128-VGPR budget
     constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
     float4 ringA0[PD][NIT], ringA1[PD][NIT];
 #pragma unroll
@@ -1045,7 +1051,7 @@ __global__ __launch_bounds__(256, OCC) void conv3x3_split3(const ConvArgs a) {
     // one burst after the last aux load: no load then waits behind an outstanding store
     // the LSTC epilogues (long-K gates convs, MT_W = 12) store in the loop instead: their
     // result registers would not fit next to the accumulators without spilling
-    constexpr bool BURST = EPI != EPI_LSTC_CELL && EPI != EPI_LSTC_OUT;
+    constexpr bool BURST = EPI != EPI_LSTC_CELL && EPI != EPI_LSTC_OUT && NWV == 4;
     float4 res[BURST ? MT_W : 1][NIT];
     float4 res1[EPI == EPI_LSTM ? MT_W : 1][NIT];         // EPI_LSTM: the cell state c (out1)
 #pragma unroll
