@@ -45,6 +45,7 @@ struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
     size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS, wU4, bU4, wUT, bU;
+    size_t w4p, b4p;                       // W0 dgrad as a four-phase conv (pack_w0phase_kernel)
     size_t total;
 };
 
@@ -82,6 +83,8 @@ Layout make_layout(const cista_config &cfg) {
     L.bU4 = off; off = align_up(off + (size_t)4 * C * 4);
     L.wUT = off; off = align_up(off + (size_t)C * C * 9 * 4);            // upsample W as [ci*9+t][co]
     L.bU = off; off = align_up(off + (size_t)C * 4);
+    L.w4p = off; off = align_up(off + (size_t)(C / 32) * 9 * (4 * C / 16) * 2 * 64 * 16);
+    L.b4p = off; off = align_up(off + (size_t)4 * C * 4);
     L.total = off;
     return L;
 }
@@ -240,7 +243,8 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
     // the epilogue indexes outputs with 32-bit element offsets (pixel * Cout, x4 for out2)
     // and the double-buffered staging reads inputs with 32-bit element offsets
-    if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 ? 4 : 1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
+    if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 || EPI == EPI_PH4 ? 4 : 1) >= (1LL << 31))
+        return CISTA_ERR_UNSUPPORTED;
     if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
     const size_t epi_lds = (size_t)NWV * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
     // + 2 x NWV words of range-pass scratch right after the epilogue's LDS (inside the dead
@@ -273,6 +277,9 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #endif
 #ifndef CISTA_ISTA8
 #define CISTA_ISTA8 0            // 1: ISTA D conv on 8-wave workgroups (measured 5 % slower), 2: also ISTA P (spills)
+#endif
+#ifndef CISTA_W0_PHASE
+#define CISTA_W0_PHASE 1         // W0's dgrad as a four-phase MFMA conv (0: the VALU dgrad_s2_kernel)
 #endif
 #ifndef CISTA_DGRAD_SMALL
 #define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
@@ -1179,7 +1186,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
     CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+    CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
+    const float *gsx = scale_of(k);                     // gx1 is final: W0's output gradient
+    if (!gsx) return CISTA_ERR_HIP;
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
     float *xfull = ws.gU, *gxfull = ws.gU;   // x_full is dead once W0's wgrad has run
     {
@@ -1192,11 +1201,30 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
     {
-        // padded-domain stride-2 dgrad into dxpF, then reflect-fold into gxfull
-        const int Hp = H + 2, Wp = W + 2, ngx = (((Wp + 1) / 2) + S2_NJ - 1) / S2_NJ;
-        hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * C * 9), dim3(256), 0, st, P.W0_w, C, C, ws.wT);
-        hipLaunchKernelGGL(dgrad_s2_kernel, g1d((long)B * Hp * 2 * ngx * (C / 8)), dim3(256), 0, st,
-                           (const float *)ws.gx1, C, 0, (const float *)ws.wT, C, C, B, h, w, ws.dxpF, Hp, Wp);
+        // padded-domain stride-2 dgrad into dxpF (split-f16 MFMA, the four output phases of a
+        // G pixel as one 4C-column conv over G, pack_w0phase_kernel), then reflect-fold into gxfull
+        int rc = CISTA_ERR_UNSUPPORTED;
+        if (CISTA_W0_PHASE) {
+            ConvArgs c;
+            memset(&c, 0, sizeof(c));
+            c.in0 = ws.gx1; c.c0 = C; c.in1 = nullptr; c.c1 = 0;
+            c.B = B; c.Hin = h; c.Win = w; c.Hout = h + 1; c.Wout = w + 1;
+            c.wpack = blob<u32x4>(k.packed, k.L.w4p);
+            c.bias = blob<float>(k.packed, k.L.b4p);
+            c.wscale = blob<float>(k.packed, k.L.sc[CV_W0]) + 1;
+            c.ascale = gsx;
+            c.N = 4 * C; c.Cout = C;
+            c.out0 = ws.dxpF;
+            rc = launch_conv<STAGE_ZP2, EPI_PH4, 1>(c, st);
+        }
+        if (rc == CISTA_ERR_UNSUPPORTED) {                 // VALU fallback
+            const int Hp = H + 2, Wp = W + 2, ngx = (((Wp + 1) / 2) + S2_NJ - 1) / S2_NJ;
+            hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * C * 9), dim3(256), 0, st, P.W0_w, C, C, ws.wT);
+            hipLaunchKernelGGL(dgrad_s2_kernel, g1d((long)B * Hp * 2 * ngx * (C / 8)), dim3(256), 0, st,
+                               (const float *)ws.gx1, C, 0, (const float *)ws.wT, C, C, B, h, w, ws.dxpF, Hp, Wp);
+            rc = hip_ok();
+        }
+        CHECK(rc);
         CHECK(fold(k, ws.dxpF, C, 0, gxfull, C, 0, C, H, W, 1.0f, 0, nullptr));
     }
     // ---- 8. We / Wi ----------------------------------------------------------------------------
@@ -1312,6 +1340,16 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
         const long dtotal = (long)(s.cout / 32) * 9 * (s.cin / 16) * 64;
         const long dgrid = dtotal > s.cin ? dtotal : s.cin;
         hipLaunchKernelGGL(pack_dgrad_kernel, dim3((unsigned)((dgrid + 255) / 256)), dim3(256), 0, st, d);
+    }
+    {   // W0's dgrad as a four-phase conv (training backward), W0's forward scale
+        PackArgs q;
+        q.w = p->W0_w; q.b = nullptr;
+        q.scale = blobw<float>(packed, L.sc[CV_W0]);
+        q.wp = blobw<u32x4>(packed, L.w4p);
+        q.bp = blobw<float>(packed, L.b4p);
+        q.Cin = C; q.Cout = 4 * C; q.G = 1;
+        const long total = (long)(C / 32) * 9 * (4 * C / 16) * 64;
+        hipLaunchKernelGGL(pack_w0phase_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, q);
     }
     const int half = C / 2;
     hipLaunchKernelGGL(transpose_small_kernel, dim3((half * nb * 9 + 255) / 256), dim3(256), 0, st,

@@ -143,6 +143,48 @@ __global__ void pack_dgrad_kernel(const PackArgs a) {
     a.wp[base + 64] = __builtin_bit_cast(u32x4, l);
 }
 
+// W0 (stride 2) dgrad as a four-phase stride-1 conv over G (conv3x3_split3<STAGE_ZP2, EPI_PH4>):
+// the padded-domain input gradient at (2i + a, 2j + b) = sum over the forward taps (dy, dx) with
+// 2y + dy = 2i + a of G(y, x) W[co][ci][dy][dx]: even rows take dy = 0 from G row i and dy = 2
+// from row i - 1, odd rows dy = 1 from row i (columns alike).  As a ZP2 correlation (output i reads
+// G rows i - 2 + ty) that is ty = 2 -> dy 0 | 1 and ty = 1 -> dy 2; the other taps are zero and
+// the kernel skips them.  B fragment: K = forward cout, column = phase (a*2+b) x forward cin; same
+// [kc][tap][ntile][part][lane] layout and per-layer scale as the forward pack (a.Cin = forward
+// Cout, a.Cout = 4 x forward Cin).
+__device__ __forceinline__ int w0_phase_tap(int parity, int t) {
+    return parity ? (t == 2 ? 1 : -1) : (t == 2 ? 0 : (t == 1 ? 2 : -1));
+}
+__global__ void pack_w0phase_kernel(const PackArgs a) {
+    const int Cf = a.Cout / 4;
+    const int NT = a.Cout / 16;
+    const int KC = a.Cin / 32;
+    const long total = (long)KC * 9 * NT * 64;
+    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    if (idx < a.Cout) a.bp[idx] = 0.0f;
+    if (idx >= total) return;
+    const int lane = (int)(idx % 64);
+    long r = idx / 64;
+    const int nt = (int)(r % NT);
+    r /= NT;
+    const int tap = (int)(r % 9);
+    const int kc = (int)(r / 9);
+    const int col = nt * 16 + (lane & 15), ph = col / Cf, ci = col - ph * Cf;
+    const int dy = w0_phase_tap(ph >> 1, tap / 3), dx = w0_phase_tap(ph & 1, tap % 3);
+    const float s = a.scale[0];
+    f16x8 h, l;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+        const int co = kc * 32 + 8 * (lane >> 4) + j;
+        const float v = (dy < 0 || dx < 0) ? 0.0f : a.w[((size_t)co * Cf + ci) * 9 + dy * 3 + dx] * s;
+        const _Float16 hb = (_Float16)v;
+        h[j] = hb;
+        l[j] = (_Float16)(v - (float)hb);
+    }
+    const size_t base = ((((size_t)kc * 9 + tap) * NT + nt) * 2) * 64 + lane;
+    a.wp[base] = __builtin_bit_cast(u32x4, h);
+    a.wp[base + 64] = __builtin_bit_cast(u32x4, l);
+}
+
 // --------------------------------------------------------------------------------------------
 // wgrad: dW[co][ci][t] (+)= sign * sum_P G(P, co) * Xpad(S*P + t, ci) on exact fp32 MFMA.
 // --------------------------------------------------------------------------------------------

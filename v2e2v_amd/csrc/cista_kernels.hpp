@@ -133,7 +133,11 @@ enum Epi {
     EPI_UP4_Q = 9,       // EPI_UP_Q of the phase-decomposed upsample conv: the output columns are
                          // (phase a*2+b, channel); a half-res pixel (i, j) yields u at the
                          // full-res pixel (2i+a, 2j+b) -- the q planes are full resolution
-    EPI_UP4_Q_SAVE = 10  // ... and stores u (out1, full-res NHWC)
+    EPI_UP4_Q_SAVE = 10, // ... and stores u (out1, full-res NHWC)
+    EPI_PH4 = 11         // out = acc: the stride-2 W0 dgrad as a four-phase conv over G (STAGE_ZP2):
+                         // packed column = (phase a*2+b, channel); phase-grid pixel (i, j) is the
+                         // padded-domain input-gradient pixel (2i+a, 2j+b) of a (2 Hout, 2 Wout)
+                         // NHWC tensor; a wave skips the taps its phase has no weight on
 };
 
 struct ConvArgs {
@@ -735,6 +739,17 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
     f16x2 amax = {};     // running max of the staged |hi| parts (the range pass below)
     const int NT = a.N >> 4;
     const int nt0 = (nblk * WN + wn) * NW;
+    // EPI_PH4: the taps of this wave's phase (a, b) (packed columns (phase, channel), NW*16 <= Cout):
+    // even phase rows read G rows i-1 (tap row 1, dy = 2) and i (tap row 2, dy = 0), odd ones row
+    // i (tap row 2, dy = 1); columns alike
+    unsigned tmask = 0x1FFu;
+    if constexpr (EPI == EPI_PH4) {
+        const int ph = (nt0 * 16) / a.Cout, pa = ph >> 1, pb = ph & 1;
+        const unsigned rows = pa ? 4u : 6u, cols = pb ? 4u : 6u;     // bit t: tap row / column t used
+        tmask = 0u;
+        for (int t = 0; t < 9; ++t)
+            if (((rows >> (t / 3)) & 1u) && ((cols >> (t % 3)) & 1u)) tmask |= 1u << t;
+    }
     const int kc0 = a.c0 >> 5;
     const int nchunks = kc0 + (a.in1 ? (a.c1 >> 5) : 0);
     const size_t tapstride = (size_t)NT * 2 * 64;   // u32x4 per tap
@@ -811,7 +826,8 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
                 __builtin_amdgcn_s_setprio(1);
 #endif
                 const int slot = CISTA_EXP_NOB ? 0 : tap % (D + 1);
-                mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
+                if (EPI != EPI_PH4 || ((tmask >> tap) & 1))
+                    mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
 #if CISTA_PRIO == 1
                 __builtin_amdgcn_s_setprio(0);
 #endif
@@ -998,7 +1014,9 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
-            if (oy < a.Hout && ox < a.Wout) v = ((b * a.Hout + oy) * a.Wout + ox) * a.Cout;
+            if (oy < a.Hout && ox < a.Wout)
+                v = EPI == EPI_PH4 ? ((b * 2 * a.Hout + 2 * oy) * 2 * a.Wout + 2 * ox) * a.Cout
+                                   : ((b * a.Hout + oy) * a.Wout + ox) * a.Cout;
         }
         ptab[p] = v;
     }
@@ -1008,6 +1026,10 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
     // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
     const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
     const int ch = ((nt0 / G) + q) * 16 + c4;              // channel within a gate
+    // store offset of the lane's channel group within a pixel's outputs (EPI_PH4: the phase's
+    // pixel of the 2 x 2 block and the channel within the phase)
+    const int chst = EPI == EPI_PH4 ? (((ch / a.Cout) >> 1) * 2 * a.Wout + ((ch / a.Cout) & 1)) * a.Cout + ch % a.Cout
+                                    : ch;
     float4 bias4[G];
 #pragma unroll
     for (int g = 0; g < G; ++g) bias4[g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + c4);
@@ -1089,7 +1111,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
                     const unsigned o = (unsigned)off + (unsigned)ch;
                     float r[4], r1[4];
                     const float *vv = reinterpret_cast<const float *>(v);
-                    if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU) {
+                    if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_PH4) {
 #pragma unroll
                         for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? relu_(vv[e]) : vv[e];
                     } else if constexpr (EPI == EPI_ISTA_D) {
@@ -1163,7 +1185,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
                     if constexpr (BURST) res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
                     else {
                         rm[it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
-                        om[it0 / 64] = off_raw < 0 ? -1 : (int)o;
+                        om[it0 / 64] = off_raw < 0 ? -1 : (int)((unsigned)off + (unsigned)chst);
                     }
                 }
             }
@@ -1194,10 +1216,10 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
 #if CISTA_NT
                 {
                     const f32x4 r4 = {res[m][it].x, res[m][it].y, res[m][it].z, res[m][it].w};
-                    __builtin_nontemporal_store(r4, (f32x4 *)(a.out0 + (unsigned)off + (unsigned)ch));
+                    __builtin_nontemporal_store(r4, (f32x4 *)(a.out0 + (unsigned)off + (unsigned)chst));
                 }
 #else
-                *(float4 *)(a.out0 + (unsigned)off + (unsigned)ch) = res[m][it];
+                *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst) = res[m][it];
 #endif
 #endif
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
