@@ -760,7 +760,8 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
 #ifndef CISTA_WG_BLOCKS
 #define CISTA_WG_BLOCKS 1024
 #endif
-constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
+constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;
+constexpr int SCL_PAIRS = 32;                // scale pairs per backward call (about 10 used)   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
@@ -804,7 +805,7 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.dlp = take((size_t)2 * C * 512);
     s.wT = take((size_t)9 * C * C);
     s.amax = reinterpret_cast<unsigned *>(take((size_t)8 * AMAX_SLOTS * AMAX_STRIDE));
-    s.scl = take(32 + 4 * nd + 4);   // 8 rotating pairs, the ISTA P / D pairs per iteration, their minima
+    s.scl = take(2 * SCL_PAIRS + 4 * nd + 4);   // the call's pairs, the ISTA P / D pairs per iteration, their minima
     s.bytes = off;
     return s;
 }
@@ -840,9 +841,51 @@ struct Bwd {
     Layout L;
     int B, H, W, h, w, C;
     hipStream_t st;
+    hipStream_t wst;        // the stream the weight gradients run on (st, or the side stream)
+    hipEvent_t evf, evj;    // fork / join events of the side stream
     BwdWs ws;
-    int slot;   // rotating scale slot
+    int slot;   // scale slot
 };
+
+// The weight gradients (wgrad + partial reduction) of a layer depend on its output gradient and
+// input only, and nothing on the backward's critical path (the dgrad chain) reads them, so they run
+// on a side stream: a one-round dgrad launch at B = 8 (one workgroup lifetime of staging, MFMAs and
+// stores, all workgroups in the same phase) then overlaps the previous layer's wgrad.  fork: the
+// side stream waits for everything the main stream has issued (the gradient, its scale); join: the
+// main stream waits for every weight gradient issued so far (before a buffer they read is reused,
+// and at the end of the call, so the call is stream-ordered for its caller).  One side stream and
+// event pair per host thread and device (created once, reentrant ABI).
+#ifndef CISTA_WGRAD_SIDE
+#define CISTA_WGRAD_SIDE 0        // 1 measured slower at B = 8 (1614 -> 1567 frames/s: the concurrent kernels contend for LDS and HBM)
+#endif
+struct SideStream { hipStream_t s = nullptr; hipEvent_t f = nullptr, j = nullptr; int dev = -1; };
+int side_stream(Bwd &k) {
+    k.wst = k.st; k.evf = k.evj = nullptr;
+    if (!CISTA_WGRAD_SIDE) return CISTA_OK;
+    thread_local SideStream ss[8];
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess) return CISTA_ERR_HIP;
+    SideStream &e = ss[dev & 7];
+    if (e.dev != dev) {
+        if (hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
+            hipEventCreateWithFlags(&e.f, hipEventDisableTiming) != hipSuccess ||
+            hipEventCreateWithFlags(&e.j, hipEventDisableTiming) != hipSuccess)
+            return CISTA_ERR_HIP;
+        e.dev = dev;
+    }
+    k.wst = e.s; k.evf = e.f; k.evj = e.j;
+    return CISTA_OK;
+}
+int side_fork(Bwd &k) {
+    if (k.wst == k.st) return CISTA_OK;
+    return hipEventRecord(k.evf, k.st) == hipSuccess && hipStreamWaitEvent(k.wst, k.evf, 0) == hipSuccess
+               ? CISTA_OK : CISTA_ERR_HIP;
+}
+int side_join(Bwd &k) {
+    if (k.wst == k.st) return CISTA_OK;
+    return hipEventRecord(k.evj, k.wst) == hipSuccess && hipStreamWaitEvent(k.st, k.evj, 0) == hipSuccess
+               ? CISTA_OK : CISTA_ERR_HIP;
+}
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
 
@@ -876,7 +919,8 @@ const float *grad_scale(Bwd &k, const float *G, long n) {
 }
 const float *scale_of(Bwd &k, float *dst) {
     unsigned *sl = scale_slots(k);
-    float *sc = dst ? dst : k.ws.scl + 2 * (k.slot & 7);
+    // pairs are not reused within a call (a weight gradient on the side stream may read one late)
+    float *sc = dst ? dst : k.ws.scl + 2 * (k.slot < SCL_PAIRS ? k.slot : SCL_PAIRS - 1);
     ++k.slot;
     hipLaunchKernelGGL(slots_scale_kernel, dim3(1), dim3(AMAX_SLOTS), 0, k.st, sl, sc);
     return hipGetLastError() == hipSuccess ? sc : nullptr;
@@ -885,7 +929,7 @@ const float *scale_of(Bwd &k, float *dst) {
 // dst (+)= sign * the split sum of the wgrad partials, and db from the bias partials, one launch
 void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, float sign, int accumulate) {
     const long nb = db ? nbias : 0;
-    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.st, (const float *)k.ws.part, ns, n,
+    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.wst, (const float *)k.ws.part, ns, n,
                        dst, sign, accumulate, (const float *)k.ws.bpart, nb, db);
 }
 
@@ -932,7 +976,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
             if (!allow_big_lds((const void *)wgrad_tr_kernel)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel, dim3(nblk, ns), dim3(512), WT_LDS, k.st, a);
+            hipLaunchKernelGGL(wgrad_tr_kernel, dim3(nblk, ns), dim3(512), WT_LDS, k.wst, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }
@@ -943,7 +987,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
         a.nsplit = ns;
         if (!allow_big_lds((const void *)wgrad_split_kernel)) return CISTA_ERR_HIP;
-        hipLaunchKernelGGL(wgrad_split_kernel, dim3(nblk, ns), dim3(256), WS_LDS, k.st, a);
+        hipLaunchKernelGGL(wgrad_split_kernel, dim3(nblk, ns), dim3(256), WS_LDS, k.wst, a);
         const long n = (long)Cout * Cin * 9;
         reduce_parts(k, ns, n, dst, db, Cout, sign, accumulate);
         return hip_ok();
@@ -957,7 +1001,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.nsplit = ns;
         switch (Cin) {
 #define WSCASE(n) \
-    case n: hipLaunchKernelGGL(wgrad_small_kernel<n>, dim3(ns), dim3(256), 0, k.st, a); break;
+    case n: hipLaunchKernelGGL(wgrad_small_kernel<n>, dim3(ns), dim3(256), 0, k.wst, a); break;
             WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6) WSCASE(7) WSCASE(8)
 #undef WSCASE
         }
@@ -976,7 +1020,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         ns = ns > ntiles ? ntiles : ns;
         ns = ns < 1 ? 1 : ns;
         a.nsplit = ns;
-        hipLaunchKernelGGL(wgrad_c1_kernel, dim3(ncb, ns), dim3(256), 0, k.st, a);
+        hipLaunchKernelGGL(wgrad_c1_kernel, dim3(ncb, ns), dim3(256), 0, k.wst, a);
         const long n = (long)Cin * 9;
         reduce_parts(k, ns, n, dst, db, 1, sign, accumulate);
         return hip_ok();
@@ -1002,7 +1046,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     const size_t lds = ((size_t)((a.TH * a.TW + 3) & ~3) + HP) * 33 * 4;
     auto kern = wgrad_kernel<XS>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
-    hipLaunchKernelGGL(kern, dim3(nblk, ns), dim3(256), lds, k.st, a);
+    hipLaunchKernelGGL(kern, dim3(nblk, ns), dim3(256), lds, k.wst, a);
     const long n = (long)Cout * Cin * 9;
     reduce_parts(k, ns, n, dst, db, Cout, sign, accumulate);
     return hip_ok();
@@ -1067,6 +1111,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
     if (g.g_rec) {
         hipLaunchKernelGGL(sigmoid_bwd_kernel, g1d(HW), dim3(256), 0, st, g.g_rec, io.rec, ws.gpre, HW);
+        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gpre, 1, 0, 1, sv.u, C, nullptr, 0, C, H, W, H, W, pg.final_w, 1.0f, 0, pg.final_b));
         DgradSmallArgs d;
         d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
@@ -1086,7 +1131,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // the dgrad below overwrites); the gradient scale is shared with that dgrad
         const float *gsu = scale_of(k);
         hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
+        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
+        CHECK(side_join(k));                            // dxpF (its X) is overwritten next
         CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
         CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
         hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C / 4), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
@@ -1102,12 +1149,14 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C, scale_slots(k));
     const float *gsc = scale_of(k);
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
     CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y, nullptr, nullptr, scale_slots(k)));   // relu(Dg) mask
     if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
     gsc = scale_of(k);
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
     CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr, g.g_z));   // g_z + fold
@@ -1123,7 +1172,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     if (hipMemsetAsync(ws.gx1, 0, (size_t)hw * C * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     const int nbl = 512;   // softshrink_bwd blocks (lambda partials [nbl][2C])
-    float *sclP = ws.scl + 32, *sclD = sclP + 2 * D;      // per-iteration scale pairs of gv / gxk
+    float *sclP = ws.scl + 2 * SCL_PAIRS, *sclD = sclP + 2 * D;      // per-iteration scale pairs of gv / gxk
     for (int it = D - 1; it >= 0; --it) {
         const float *v = sv.v + (size_t)it * hw * 2 * C;
         float *gv = ws.gv + (size_t)it * hw * 2 * C, *gxk = ws.gxk + (size_t)it * hw * C;
@@ -1158,6 +1207,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         float *sP = sclD + 2 * D, *sD = sP + 2;
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclP, D, sP);
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclD, D, sD);
+        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0, pg.P_b, sP,
                            D * B));
         CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, ws.zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
@@ -1165,11 +1215,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------
     // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part)
+    CHECK(side_join(k));                                // Gl (the LSTM wgrad's G) is overwritten next
     hipLaunchKernelGGL(lstc_bwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st, (const float *)sv.gi,
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C, scale_slots(k, 0), scale_slots(k, 1));
     gsc = scale_of(k);                                   // Go; Gl's scale is the next slot set
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
     CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp, gsc));
@@ -1178,12 +1230,14 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
     gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
     CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
     CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
@@ -1199,6 +1253,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         f.need_full = true;
         CHECK(run_layer(f, CISTA_LAYER_INPUT));
     }
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
     {
         // padded-domain stride-2 dgrad into dxpF (split-f16 MFMA, the four output phases of a
@@ -1225,10 +1280,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
             rc = hip_ok();
         }
         CHECK(rc);
+        CHECK(side_join(k));                            // gxfull overwrites x_full (W0's wgrad X)
         CHECK(fold(k, ws.dxpF, C, 0, gxfull, C, 0, C, H, W, 1.0f, 0, nullptr));
     }
     // ---- 8. We / Wi ----------------------------------------------------------------------------
     const int half = C / 2, nb = k.cfg->num_bins;
+    CHECK(side_fork(k));
     CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0, pg.We_b));
     CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0,
                          pg.Wi_b));
@@ -1251,6 +1308,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.Cin = nb; d.accumulate = 0;
         hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * nb), dim3(256), 0, st, d);
     }
+    CHECK(side_join(k));                                // the caller's stream waits for every wgrad
     return hip_ok();
 }
 }  // namespace
@@ -1580,6 +1638,7 @@ int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float
     k.st = static_cast<hipStream_t>(stream);
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
+    k.wst = k.st; k.evf = k.evj = nullptr;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     const int C = k.C;
     return wgrad<XS_S1>(k, G, 2 * C, 0, 2 * C, X, C, nullptr, 0, C, k.h, k.w, k.h, k.w, dW, 1.0f, 0, db, gscale,
@@ -1640,6 +1699,7 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
+    CHECK(side_stream(k));
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
     if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
         return CISTA_ERR_HIP;
