@@ -434,12 +434,14 @@ def time_voxelizer(torch, n_windows, n_events, nb, H, W, device, reps=5, cpu_leg
     from v2e2v_amd import event_process as ep
     ev, off = synth_events(torch, n_windows, n_events, H, W, 99, device)
     out = torch.empty(n_windows, nb, H, W, device=device)
-    ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device)
+    ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device,
+                             strict=False)
     torch.cuda.synchronize()
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device)
+        ep.events_to_voxel_batch((ev, off), nb, W, H, mode="std", filter_hot_pixel=True, out=out, device=device,
+                                 strict=False)
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps

@@ -47,6 +47,17 @@ enum {
                                 float64 events tensor) instead of numpy's np.add.at           */
 };
 
+/* grid_status bits of cista_voxelize_checked: what the reference does with an event outside the
+ * H x W frame (its np.add.at on the flat index x + y W + bin H W, utils/event_process.py:53-58) */
+enum {
+    CISTA_VOXEL_OUT_OF_RANGE = 1,  /* a flat index (np.uint: truncated, wrapped modulo 2^64, read
+                                      back as intp) outside [-size, size): the reference raises
+                                      IndexError                                                */
+    CISTA_VOXEL_SPILL = 2          /* a flat index inside [-size, size): the reference adds the
+                                      event to another pixel / bin (a negative index counts from
+                                      the end of the grid); this build drops it                  */
+};
+
 /* Workspace for cista_voxelize: n_events = total events of the batch (offsets[B]). */
 size_t cista_voxel_workspace_bytes(int B, long long n_events, int num_bins, int height, int width);
 
@@ -60,12 +71,20 @@ size_t cista_voxel_workspace_bytes(int B, long long n_events, int num_bins, int 
  * mode     : CISTA_VOXEL_*; hot_threshold > 0 zeroes |v| > hot_threshold before normalising
  *            (reference: 25/num_bins for event_preprocess(filter_hot_pixel=True),
  *            20/num_bins for event_preprocess_pytorch); <= 0 disables the filter.
- * Events whose x, y fall outside the grid are dropped (the reference raises IndexError).
- * The input is never modified (the reference rewrites events[:, 0] and the polarity column).
+ * Events whose x, y fall outside the H x W frame are dropped; cista_voxelize_checked reports
+ * them (grid_status).  The input is never modified (the reference rewrites events[:, 0] and the
+ * polarity column).
  */
 int cista_voxelize(const double *events, const long long *offsets, int B, long long n_events, int num_bins,
                    int height, int width, int mode, float hot_threshold, float *voxels, void *workspace,
                    size_t workspace_bytes, void *stream);
+
+/* cista_voxelize that also ORs CISTA_VOXEL_OUT_OF_RANGE / CISTA_VOXEL_SPILL into *grid_status (a
+ * DEVICE int the caller zeroes; NULL = no report) for the events outside the frame, so that a
+ * caller can raise where the reference raises (read it after the stream has run the call). */
+int cista_voxelize_checked(const double *events, const long long *offsets, int B, long long n_events, int num_bins,
+                           int height, int width, int mode, float hot_threshold, float *voxels, void *workspace,
+                           size_t workspace_bytes, int *grid_status, void *stream);
 
 /* event_preprocess alone, in place, on B existing (num_bins, height, width) float32 voxel grids
  * (reference utils/event_process.py:132-154 / :157-176); workspace from

@@ -77,9 +77,41 @@ def test_edge_cases():
                     [0.04, -0.5, 3, 1], [0.05, 5, 5, 1]], np.float64)
     ev1_kept = ev1[[0, 1, 4, 5]].copy()
     ev1_kept[2, 1] = 0.0                         # -0.5 truncates to 0, like the reference's cast
-    got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H).cpu().numpy()
+    # x = W and y = H are inside the flat grid: the reference adds them to other pixels / bins,
+    # this build drops them and says so
+    with pytest.warns(RuntimeWarning, match="dropped"):
+        got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H).cpu().numpy()
     assert_bits(got[0], ref_raw(ev0, nb, W, H))
     assert_bits(got[1], ref_raw(ev1_kept, nb, W, H))
+    got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H, strict=False).cpu().numpy()   # no check
+    assert_bits(got[1], ref_raw(ev1_kept, nb, W, H))
+
+
+@pytest.mark.parametrize("bad", ["negative_x", "beyond_grid", "last_bin_row_below"])
+def test_out_of_grid_raises_like_reference(bad):
+    """np.add.at on the flat index x + y W + bin H W (utils/event_process.py:53-58) raises
+    IndexError once an index reaches the grid size; the GPU path raises there too (both the fused
+    per-window path and, for a large frame, the global-sort path)."""
+    nb = 5
+    for H, W in ((20, 30), (520, 520)):          # 520 x 520 >= 2^18 pixels: the keys + hipCUB path
+        ev = np.array([[0.0, 2, 3, 1], [0.01, 5, 5, 0], [0.02, 7, 1, 1], [0.04, 1, 1, 1]], np.float64)
+        if bad == "negative_x":
+            ev[0, 1:3] = (-(nb * H * W + 7.0), 0.0)   # np.uint wraps; as intp below -size
+        elif bad == "beyond_grid":
+            ev[2, 2] = H * nb + 3                # y far below the frame: past the last bin
+        else:
+            ev[3, 2] = H                         # last event -> last bin, one row below the frame
+        with pytest.raises(IndexError):
+            fx.voxelize(ev, nb, W, H)            # the reference's behaviour (oracle restatement)
+        with pytest.raises(IndexError):
+            ep.events_to_voxel_batch([ev], nb, W, H)
+        ep.events_to_voxel_batch([ev], nb, W, H, strict=False)     # unchecked: the event is dropped
+    # a negative x whose flat index stays inside [-size, size) lands elsewhere in the reference
+    # (moved back a row, or counted from the end of the grid): a spill
+    ev = np.array([[0.0, -3, 0, 1], [0.01, -3, 5, 0], [0.04, 1, 1, 1]], np.float64)
+    fx.voxelize(ev, nb, 30, 20)
+    with pytest.warns(RuntimeWarning, match="dropped"):
+        ep.events_to_voxel_batch([ev], nb, 30, 20)
 
 
 def test_preprocess_thresholds_and_batch_shapes():

@@ -111,6 +111,8 @@ def _declare(lib):
         "cista_voxel_workspace_bytes": (c_size_t, [c_int, ctypes.c_longlong, c_int, c_int, c_int]),
         "cista_voxelize": (c_int, [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_int, c_int, c_int,
                                    ctypes.c_float, c_void_p, c_void_p, c_size_t, c_void_p]),
+        "cista_voxelize_checked": (c_int, [c_void_p, c_void_p, c_int, ctypes.c_longlong, c_int, c_int, c_int, c_int,
+                                   ctypes.c_float, c_void_p, c_void_p, c_size_t, c_void_p, c_void_p]),
         "cista_voxel_preprocess": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_int, ctypes.c_float,
                                            c_void_p, c_size_t, c_void_p]),
         # include/cista_loss.h (config struct passed as a pointer; see losses.CistaSsimConfig)

@@ -58,8 +58,32 @@ __device__ __forceinline__ int window_of(const long long *off, int B, long long 
     return lo;
 }
 
+// Reference :53-58: np.add.at on the flat index x + y W + bin H W raises IndexError when an index
+// reaches the grid size, and otherwise adds an event outside the H x W frame to another pixel (or
+// bin).  Such an event is dropped here; this records which of the two the reference does with it:
+// CISTA_VOXEL_OUT_OF_RANGE (it raises) or CISTA_VOXEL_SPILL (it writes elsewhere).  Called for the
+// events outside the frame only (rare).  x, y as np.uint: truncated toward zero and wrapped
+// modulo 2^64 (float -3.0 -> 2^64 - 3), and np.add.at reads the uint64 index as intp, so the sum
+// is a signed index: in [-size, size) it is valid (a negative one counts from the end of the
+// grid, Python-style), outside it raises.
+__device__ __noinline__ void grid_status(const double *e, double x, double y, double first, double dT, int nb,
+                                         int H, int W, bool torch_floor, int *status) {
+    const double ts = (double)(nb - 1) * (e[0] - first) / dT;
+    const double tf = torch_floor ? floor(ts) : ts;
+    if (!(tf > -1.0) || !(tf < 9.0e18) || (torch_floor && tf < 0.0)) return;   // hits no bin
+    const long long ti = (long long)tf;
+    const long long HW = (long long)H * W, size = (long long)nb * HW;
+    const bool huge = !(fabs(x) < 1.0e15) || !(fabs(y) < 1.0e15);            // NaN / inf included
+    const long long flat = huge ? 0 : (long long)x + (long long)y * W;      // trunc, signed
+    auto bad = [&](long long i) { return huge || i < -size || i >= size; };
+    int f = 0;
+    if (ti < nb) f |= bad(flat + ti * HW) ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
+    if (ti + 1 < nb) f |= bad(flat + (ti + 1) * HW) ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
+    if (f) atomicOr(status, f);
+}
+
 __global__ void vox_keys_kernel(const double *ev, const long long *off, int B, long long N, int H, int W,
-                                unsigned long long *keys, int *vals) {
+                                unsigned long long *keys, int *vals, int nb, int torch_acc, int *status) {
     const long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= N) return;
     const int b = window_of(off, B, i);
@@ -69,6 +93,12 @@ __global__ void vox_keys_kernel(const double *ev, const long long *off, int B, l
     // reference :42-43: astype(np.uint) truncates toward zero, so (-1, W) maps into [0, W)
     if (x > -1.0 && x < (double)W && y > -1.0 && y < (double)H)
         key = (unsigned long long)b * HW + (unsigned long long)y * W + (unsigned long long)x;
+    else if (status) {
+        const long long e0 = off[b], e1 = off[b + 1] - 1;
+        double dT = ev[4 * e1] - ev[4 * e0];
+        if (dT == 0.0) dT = 1.0;
+        grid_status(ev + 4 * i, x, y, ev[4 * e0], dT, nb, H, W, torch_acc != 0, status);
+    }
     keys[i] = key;
     vals[i] = (int)i;
 }
@@ -206,7 +236,8 @@ __device__ __forceinline__ int key_lower(const unsigned *k, int n, unsigned p) {
 // grid (B), block WT, dynamic LDS sizeof(WinLds).  scratch: n_events sorted keys (window b's
 // segments at its event offsets); tb: TBMAX + 1 tile starts per window (single-segment windows)
 __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const long long *off, int nb, int H, int W,
-                                                      int end_bit, unsigned *scratch, double2 *tp_sorted, int *tb) {
+                                                      int end_bit, unsigned *scratch, double2 *tp_sorted, int *tb,
+                                                      int torch_acc, int *status) {
     extern __shared__ __align__(16) char wsm[];
     WinLds &L = *reinterpret_cast<WinLds *>(wsm);
     const int b = blockIdx.x, tid = threadIdx.x;
@@ -236,6 +267,11 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
                 // reference :42-43: astype(np.uint) truncates toward zero
                 const bool in = l < cnt && x[i] > -1.0 && x[i] < (double)W && y[i] > -1.0 && y[i] < (double)H;
                 key[i0 + i] = in ? ((((unsigned)y[i] * (unsigned)W + (unsigned)x[i]) << 14) | (unsigned)l) : 0xFFFFFFFFu;
+                if (__builtin_expect(status && l < cnt && !in, 0)) {
+                    double dT = ev[4 * (e0 + n - 1)] - ev[4 * e0];
+                    if (dT == 0.0) dT = 1.0;
+                    grid_status(ev + 4 * (base + l), x[i], y[i], ev[4 * e0], dT, nb, H, W, torch_acc != 0, status);
+                }
             }
         }
         __syncthreads();                                                // LDS union reuse
@@ -957,6 +993,13 @@ size_t cista_voxel_workspace_bytes(int B, long long n_events, int num_bins, int 
 int cista_voxelize(const double *events, const long long *offsets, int B, long long n_events, int num_bins,
                    int height, int width, int mode, float hot_threshold, float *voxels, void *workspace,
                    size_t workspace_bytes, void *stream) {
+    return cista_voxelize_checked(events, offsets, B, n_events, num_bins, height, width, mode, hot_threshold, voxels,
+                                  workspace, workspace_bytes, nullptr, stream);
+}
+
+int cista_voxelize_checked(const double *events, const long long *offsets, int B, long long n_events, int num_bins,
+                           int height, int width, int mode, float hot_threshold, float *voxels, void *workspace,
+                           size_t workspace_bytes, int *grid_status, void *stream) {
     if (B < 0 || n_events < 0 || n_events > 0x7fffffffLL || num_bins <= 0 || height <= 0 || width <= 0)
         return CISTA_ERR_INVALID;
     const int torch_acc = (mode & CISTA_VOXEL_TORCH_ACCUM) != 0;
@@ -978,7 +1021,7 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
         int *tb = reinterpret_cast<int *>(w.tb);
         double2 *tps = reinterpret_cast<double2 *>(w.tps);
         hipLaunchKernelGGL(vox_sort_kernel, dim3(B), dim3(WT), sizeof(WinLds), st, events, offsets, num_bins, height,
-                           width, 14 + end_bits(HW), scr, tps, tb);
+                           width, 14 + end_bits(HW), scr, tps, tb, torch_acc, grid_status);
         hipLaunchKernelGGL(torch_acc ? vox_tile_kernel<true> : vox_tile_kernel<false>, dim3(ntiles, B), dim3(TT), 0,
                            st, events, offsets, num_bins, height, width, (const unsigned *)scr, (const double2 *)tps,
                            (const int *)tb, voxels);
@@ -988,7 +1031,7 @@ int cista_voxelize(const double *events, const long long *offsets, int B, long l
     if (hipMemsetAsync(voxels, 0, (size_t)B * n * sizeof(float), st) != hipSuccess) return CISTA_ERR_HIP;
     if (n_events > 0) {
         hipLaunchKernelGGL(vox_keys_kernel, g1d(n_events), dim3(256), 0, st, events, offsets, B, n_events, height,
-                           width, w.k0, w.v0);
+                           width, w.k0, w.v0, num_bins, torch_acc, grid_status);
         size_t cb = w.cub_bytes;
         const int bits = end_bits((unsigned long long)B * height * width);
         if (hipcub::DeviceRadixSort::SortPairs(w.cub, cb, (const unsigned long long *)w.k0, w.k1,

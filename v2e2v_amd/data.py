@@ -238,12 +238,17 @@ class GpuVoxelLoader:
     Data parallel (config c4): with world_size > 1 -- given, or taken from the initialised
     torch.distributed group -- the loader reads only this rank's SequenceShardSampler shard and
     ``batch_size`` is the per-rank batch (global batch = world_size x batch_size).  ``shuffle``
-    then goes to the sampler (same permutation on every rank); call ``set_epoch`` each epoch."""
+    then goes to the sampler (same permutation on every rank); call ``set_epoch`` each epoch.
+
+    ``strict`` (default): an event file with events outside the frame fails like the reference's
+    dataset does (IndexError from np.add.at; see event_process.events_to_voxel_batch) -- one
+    stream synchronisation per batch."""
 
     def __init__(self, dataset: TrainFixNEventData, device, rank: int | None = None, world_size: int | None = None,
-                 shuffle: bool = False, seed: int = 0, **loader_kwargs):
+                 shuffle: bool = False, seed: int = 0, strict: bool = True, **loader_kwargs):
         self.ds = dataset
         self.device = torch.device(device)
+        self.strict = bool(strict)
         if world_size is None:
             dd = torch.distributed
             world_size = dd.get_world_size() if dd.is_available() and dd.is_initialized() else 1
@@ -298,7 +303,8 @@ class GpuVoxelLoader:
             events = torch.cat(evs, 0) if evs else torch.zeros(0, 4, dtype=torch.float64)
             offsets = torch.tensor(np.concatenate([[0], np.cumsum(sizes)]), dtype=torch.int64)
             vox = ep.events_to_voxel_batch((events.to(self.device), offsets), self.ds.num_bins, self.ds.width,
-                                           self.ds.height, mode="std", filter_hot_pixel=False, device=self.device)
+                                           self.ds.height, mode="std", filter_hot_pixel=False, device=self.device,
+                                           strict=self.strict)
             B = len(items)
             vox = vox.view(L, B, self.ds.num_bins, self.ds.height, self.ds.width)
             if self.ds.add_noise:

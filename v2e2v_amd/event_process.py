@@ -23,6 +23,7 @@ IndexError.  There is no CPU fallback: without the HIP library every call raises
 from __future__ import annotations
 
 import ctypes
+import warnings
 
 import numpy as np
 import torch
@@ -32,6 +33,7 @@ from . import _lib
 MODES = {"none": 0, "raw": 0, "std": 1, "maxmin": 2}
 STD_F32 = 3                 # CISTA_VOXEL_STD_F32: event_preprocess_pytorch's float32 statistics
 TORCH_ACCUM = 0x10          # CISTA_VOXEL_TORCH_ACCUM: events_to_voxel_grid_pytorch accumulation
+OUT_OF_RANGE, SPILL = 1, 2  # cista_voxelize_checked grid_status bits (include/cista_voxel.h)
 _ws_cache: dict = {}
 
 
@@ -66,7 +68,8 @@ def _threshold(filter_hot_pixel: bool, num_bins: int, per_bin: float) -> float:
 
 def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode: str = "none",
                           filter_hot_pixel: bool = False, hot_threshold: float | None = None,
-                          out: torch.Tensor | None = None, device=None, torch_semantics: bool = False) -> torch.Tensor:
+                          out: torch.Tensor | None = None, device=None, torch_semantics: bool = False,
+                          strict: bool = True) -> torch.Tensor:
     """Voxelize (and optionally normalise) B event windows at once.
 
     ``windows`` is either a list of [N_b x 4] arrays/tensors (t, x, y, p), or a pair
@@ -75,6 +78,12 @@ def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode:
     ``filter_hot_pixel`` uses the numpy threshold 25/num_bins unless ``hot_threshold`` is given.
     ``torch_semantics``: the torch twins' arithmetic (events_to_voxel_grid_pytorch accumulation,
     event_preprocess_pytorch float32 'std' statistics) instead of the numpy path's.
+    ``strict`` (default): events outside the H x W frame are checked the way the reference's
+    ``np.add.at`` on the flat index treats them (utils/event_process.py:53-58): an index past the
+    grid raises IndexError as there; an event the reference would add to another pixel or bin
+    (x >= W or y >= H at a flat index inside the grid) is dropped here and reported with a
+    RuntimeWarning.  Costs one stream synchronisation; ``strict=False`` skips it (such events are
+    dropped silently).
     Returns (B, num_bins, height, width) float32 on the GPU.
     """
     if num_bins <= 0 or width <= 0 or height <= 0:
@@ -102,10 +111,22 @@ def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode:
     L = _lib.lib()
     nbytes = L.cista_voxel_workspace_bytes(B, N, num_bins, height, width)
     ws = _workspace(dev, nbytes)
+    status = torch.zeros(1, dtype=torch.int32, device=dev) if strict else None
     with torch.cuda.device(dev):
-        _lib.check(L.cista_voxelize(_lib.ptr(events) if N else None, offsets.data_ptr(), B, N, num_bins, height,
-                                    width, m, ctypes.c_float(thr), out.data_ptr(), ws.data_ptr(),
-                                    ws.numel(), _lib.stream_handle(dev)), "cista_voxelize")
+        _lib.check(L.cista_voxelize_checked(_lib.ptr(events) if N else None, offsets.data_ptr(), B, N, num_bins,
+                                            height, width, m, ctypes.c_float(thr), out.data_ptr(), ws.data_ptr(),
+                                            ws.numel(), _lib.ptr(status), _lib.stream_handle(dev)),
+                   "cista_voxelize_checked")
+    if strict:
+        flags = int(status.item())
+        if flags & OUT_OF_RANGE:
+            raise IndexError(f"index out of bounds for a voxel grid of size {num_bins * height * width}: an event's "
+                             f"x, y lie outside the {height}x{width} frame (np.add.at raises here, "
+                             "utils/event_process.py:53-58)")
+        if flags & SPILL:
+            warnings.warn(f"events outside the {height}x{width} frame were dropped; the reference adds them "
+                          "to another pixel or bin (np.add.at on the flat index x + y*W + bin*H*W)",
+                          RuntimeWarning, stacklevel=2)
     return out
 
 
