@@ -760,8 +760,8 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
 #ifndef CISTA_WG_BLOCKS
 #define CISTA_WG_BLOCKS 1024
 #endif
-constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;
-constexpr int SCL_PAIRS = 32;                // scale pairs per backward call (about 10 used)   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
+constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
+constexpr int SCL_PAIRS = 16;                // scale pairs of the non-ISTA gradients of a call (8 used)
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
@@ -844,7 +844,8 @@ struct Bwd {
     hipStream_t wst;        // the stream the weight gradients run on (st, or the side stream)
     hipEvent_t evf, evj;    // fork / join events of the side stream
     BwdWs ws;
-    int slot;   // scale slot
+    int slot;   // |max| slot set (rotating over 8)
+    int pair;   // next scale pair of the call (never reused within a call)
 };
 
 // The weight gradients (wgrad + partial reduction) of a layer depend on its output gradient and
@@ -920,7 +921,11 @@ const float *grad_scale(Bwd &k, const float *G, long n) {
 const float *scale_of(Bwd &k, float *dst) {
     unsigned *sl = scale_slots(k);
     // pairs are not reused within a call (a weight gradient on the side stream may read one late)
-    float *sc = dst ? dst : k.ws.scl + 2 * (k.slot < SCL_PAIRS ? k.slot : SCL_PAIRS - 1);
+    float *sc = dst;
+    if (!sc) {
+        if (k.pair >= SCL_PAIRS) return nullptr;        // more gradients than the workspace has pairs for
+        sc = k.ws.scl + 2 * k.pair++;
+    }
     ++k.slot;
     hipLaunchKernelGGL(slots_scale_kernel, dim3(1), dim3(AMAX_SLOTS), 0, k.st, sl, sc);
     return hipGetLastError() == hipSuccess ? sc : nullptr;
@@ -1638,6 +1643,7 @@ int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float
     k.st = static_cast<hipStream_t>(stream);
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
+    k.pair = 0;
     k.wst = k.st; k.evf = k.evj = nullptr;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     const int C = k.C;
@@ -1698,6 +1704,7 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     k.st = static_cast<hipStream_t>(stream);
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
+    k.pair = 0;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     CHECK(side_stream(k));
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
