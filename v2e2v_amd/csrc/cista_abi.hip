@@ -113,7 +113,7 @@ struct Workspace {
 };
 
 // every workspace (inference, training forward, backward) starts with this reserved header:
-// its first int32 is the range flag, which no carve hands out as scratch
+// (reserved: ABI versions <= 2 kept a range flag there), which no carve hands out as scratch
 constexpr size_t WS_HEADER = ALIGN;
 
 Workspace carve(void *ws, int B, int H, int W, int C) {
@@ -776,7 +776,7 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     const int h = H / 2, w = W / 2, C = cfg.base_channels;
     const size_t hw = (size_t)B * h * w, HW = (size_t)B * H * W;
     BwdWs s;
-    size_t off = WS_HEADER;    // the range flag survives the backward's use of the buffer
+    size_t off = WS_HEADER;    // the reserved header is never handed out as scratch
     char *base = static_cast<char *>(buf);
     auto take = [&](size_t nfloat) {
         float *p = reinterpret_cast<float *>(base + off);

@@ -14,7 +14,8 @@
 //    ~fp32 accuracy: 3e-6 vs the fp64 truth on the stress fixture's LSTM state, where a
 //    bf16 split measured 1.5e-4.  Weights are pre-scaled by a per-layer
 //    power of two so their lo part stays normal; the epilogue undoes it exactly.
-//    Activations must satisfy |x| < 65504 (fp16 range); larger values surface as inf/NaN;
+//    a tile whose staged input does not fit the fp16 hi part (|x| >= 65520) is recomputed in the
+//    same launch with a power-of-two pre-scale (the range pass below);
 //  * weights are pre-packed once per parameter update into per-lane MFMA B fragments
 //    (hi and lo), read straight from L2 into VGPRs with 1 KiB coalesced loads;
 //  * every elementwise op of the reference (bias, ReLU, sigmoid/tanh gate algebra, the
@@ -54,7 +55,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_EXP_SMALLSTORE
 #define CISTA_EXP_SMALLSTORE 0     // != 0: store offsets masked into a small window (value = mask)
 #endif
-// CISTA_RANGE_CHECK=0 compiles the fp16-range flag out of the staging (A/B of its cost)
+// CISTA_RANGE_CHECK=0 compiles the fp16-range check (and the range pass) out of the staging (A/B)
 #ifndef CISTA_RANGE_CHECK
 #define CISTA_RANGE_CHECK 1
 #endif
@@ -213,7 +214,7 @@ __device__ __forceinline__ float softshrink_(float x, float l) { return relu_(x 
 
 // split 8 fp32 into fp16 hi and lo (x ~= hi + lo, residual <= 2^-22 |x| + 2^-25); hmax
 // keeps the running packed max of |hi|: it reaches inf exactly when a staged |x| >= 65520
-// does not fit the fp16 hi part (the range flag; 4 packed v_pk_max_f16 per 8 values)
+// does not fit the fp16 hi part (the range pass's trigger; 4 packed v_pk_max_f16 per 8 values)
 typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void split8(const float4 &a, const float4 &b, u32x4 &hi, u32x4 &lo, f16x2 &hmax) {
     float v[8] = {a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
