@@ -991,12 +991,30 @@ __global__ __launch_bounds__(256) void wgrad_c1_kernel(const WgradArgs a) {
             d[0] = v.x; d[1] = v.y; d[2] = v.z; d[3] = v.w;
         }
         __syncthreads();
-        for (int p = ph; p < 256; p += 8) {
-            const float g = gs[p];
-            if (blockIdx.x == 0 && ci == 0) bsum += g;
-            const int hb = (p >> 4) * 18 + (p & 15);
+        // phase ph walks tile rows 2ph, 2ph+1 left to right with the 3 x 3 input window of its
+        // channel in registers: 3 LDS reads per pixel instead of 9
 #pragma unroll
-            for (int t = 0; t < 9; ++t) acc[t] = fmaf(g, Xs[(hb + (t / 3) * 18 + (t % 3)) * 33 + ci], acc[t]);
+        for (int rr = 0; rr < 2; ++rr) {
+            const int py = 2 * ph + rr;
+            float w[3][3];
+#pragma unroll
+            for (int dy = 0; dy < 3; ++dy) {
+                w[dy][1] = Xs[((py + dy) * 18 + 0) * 33 + ci];
+                w[dy][2] = Xs[((py + dy) * 18 + 1) * 33 + ci];
+            }
+#pragma unroll 4
+            for (int px = 0; px < 16; ++px) {
+#pragma unroll
+                for (int dy = 0; dy < 3; ++dy) {
+                    w[dy][0] = w[dy][1];
+                    w[dy][1] = w[dy][2];
+                    w[dy][2] = Xs[((py + dy) * 18 + px + 2) * 33 + ci];
+                }
+                const float g = gs[py * 16 + px];
+                if (blockIdx.x == 0 && ci == 0) bsum += g;
+#pragma unroll
+                for (int t = 0; t < 9; ++t) acc[t] = fmaf(g, w[t / 3][t % 3], acc[t]);
+            }
         }
     }
     __syncthreads();
@@ -1057,14 +1075,36 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradArgs a) {
             Xh[i] = a.X0[(((size_t)b * a.x0c + c) * a.Hin + y) * a.Win + x];
         }
         __syncthreads();
-        for (int p = ph; p < 256; p += 8) {
-            const float g = Gt[p * 33 + co];
-            bsum += g;
-            const int hb = (p >> 4) * 18 + (p & 15);
+        // phase ph walks tile rows 2ph, 2ph+1 left to right with the CI x 3 x 3 input window in
+        // registers (wave-uniform: LDS broadcasts): 3 CI reads per pixel instead of 9 CI
+#pragma unroll
+        for (int rr = 0; rr < 2; ++rr) {
+            const int py = 2 * ph + rr;
+            float w[CI][3][3];
 #pragma unroll
             for (int c = 0; c < CI; ++c)
 #pragma unroll
-                for (int t = 0; t < 9; ++t) acc[c][t] = fmaf(g, Xh[c * 324 + hb + (t / 3) * 18 + (t % 3)], acc[c][t]);
+                for (int dy = 0; dy < 3; ++dy) {
+                    w[c][dy][1] = Xh[c * 324 + (py + dy) * 18 + 0];
+                    w[c][dy][2] = Xh[c * 324 + (py + dy) * 18 + 1];
+                }
+#pragma unroll 2
+            for (int px = 0; px < 16; ++px) {
+#pragma unroll
+                for (int c = 0; c < CI; ++c)
+#pragma unroll
+                    for (int dy = 0; dy < 3; ++dy) {
+                        w[c][dy][0] = w[c][dy][1];
+                        w[c][dy][1] = w[c][dy][2];
+                        w[c][dy][2] = Xh[c * 324 + (py + dy) * 18 + px + 2];
+                    }
+                const float g = Gt[(py * 16 + px) * 33 + co];
+                bsum += g;
+#pragma unroll
+                for (int c = 0; c < CI; ++c)
+#pragma unroll
+                    for (int t = 0; t < 9; ++t) acc[c][t] = fmaf(g, w[c][t / 3][t % 3], acc[c][t]);
+            }
         }
     }
     // sum the 8 phases in order 0..7 (phase 0 accumulates the others through LDS)
