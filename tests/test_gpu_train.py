@@ -195,3 +195,36 @@ def test_c3_batch8_bptt_against_fp64_truth(golden):
     print("\n" + "\n".join(f"  c3 B=8 grad {k:40s} hip-vs-f64 {e:.2e}   ref32-vs-f64 {n:.2e}"
                             for k, e, n in sorted(rows, key=lambda r: -r[1])[:6]))
     assert not bad, bad
+
+
+@pytest.mark.parametrize("xscale", [1.0, 3.0e5])
+def test_wgrad_tr_kernel_matches_fp64(xscale):
+    """The split-f16 weight-gradient kernel on its own (the backward's stacked ISTA P launch,
+    cista_wgrad_ista_p: wgrad_tr_kernel + reduce_partials_kernel) against an fp64 conv weight
+    gradient over the reflect-padded input: dW = sum_P G(P) x Xpad(P + t), db = sum_P G(P).
+    xscale = 3e5 puts the activations beyond the fp16 hi part, so every tile takes the re-staging
+    path with a power-of-two pre-scale (X has no per-tensor scale); the bar stays fp32-level."""
+    import ctypes
+    from v2e2v_amd import _lib
+    C, D, B, H, W = 64, 5, 2, 36, 52              # ragged tiles: 18 x 26 half-res, 6 x 16 tiles
+    h, w = H // 2, W // 2
+    m = CistaLSTCNet([H, W], base_channels=C, depth=D, num_bins=5).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    G = torch.rand(D * B, h, w, 2 * C, device=DEV, generator=g) * 2 - 1
+    X = (torch.rand(D * B, h, w, C, device=DEV, generator=g) * 2 - 1) * xscale
+    sc = torch.tensor([8192.0, 1.0 / 8192.0], device=DEV)        # max |G s| <= 16384
+    dW = torch.empty(2 * C, C, 3, 3, device=DEV)
+    db = torch.empty(2 * C, device=DEV)
+    ws = m.train_workspace(B, H, W, DEV)
+    L = _lib.lib()
+    cfg = m._cfg()
+    _lib.check(L.cista_wgrad_ista_p(ctypes.byref(cfg), B, H, W, G.data_ptr(), X.data_ptr(), sc.data_ptr(),
+                                    dW.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
+                                    torch.cuda.current_stream().cuda_stream), "cista_wgrad_ista_p")
+    torch.cuda.synchronize()
+    Gd = G.double().permute(0, 3, 1, 2)
+    Xd = torch.nn.functional.pad(X.double().permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect")
+    ref = torch.nn.grad.conv2d_weight(Xd, (2 * C, C, 3, 3), Gd)
+    # fp32 accumulation over 4680 pixels: ~sqrt(N) x 6e-8 of the largest entry
+    assert rel_err(dW.double().cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
