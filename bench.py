@@ -163,6 +163,19 @@ def v2e2v_main(args, torch, vd, rank, world, device):
         e1.record()
         e1.synchronize()
         v2e_ms = e0.elapsed_time(e1) / reps
+        # output_mode='raw' on the same packs: count pass + row pass, one host sync per call
+        from v2e2v_amd.v2e import EventEmulator
+        raw = EventEmulator("raw", num_bins=cfgs.num_bins, pos_thres=cfgs.C, neg_thres=cfgs.C,
+                            sigma_thres=cfgs.threshold_sigma, cutoff_hz=cfgs.cutoff_hz,
+                            refractory_period_s=cfgs.refractory_period_s, leak_rate_hz=0.1, shot_noise_rate_hz=1,
+                            device=device, seed=5)
+        raw(frames, ts0)
+        t_raw = time.perf_counter()
+        raw_events = 0
+        for r in range(reps):
+            raw_events += raw(frames, ts0 + (r + 1) * P * dt)[1]
+        torch.cuda.synchronize()
+        raw_ms = (time.perf_counter() - t_raw) * 1e3 / reps
     cpu = None
     if rank == 0 and not args.no_cpu_baseline:
         cpu = v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt)
@@ -180,6 +193,8 @@ def v2e2v_main(args, torch, vd, rank, world, device):
             "events_last_pack": int(net.num_events), "outputs_finite": bool(torch.isfinite(rec).all()),
             "roofline": roofline, "cpu_baseline": cpu,
             "emulator_ms_per_pack": round(v2e_ms, 4),
+            "emulator_raw_mode": {"ms_per_pack": round(raw_ms, 4), "events_per_pack": raw_events // reps,
+                                  "events_per_s": round(raw_events / (raw_ms * reps / 1e3), 1)},
             "reconstruction_ms_per_frame_kernels": round(sum(v["ms"] * v["launches_per_frame"]
                                                              for v in layers.values()), 4),
             "layers_ms": {k: round(v["ms"], 4) for k, v in layers.items()}}),

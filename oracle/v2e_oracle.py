@@ -159,11 +159,12 @@ class NoRandom:
 
 
 class V2EOracle:
-    """EventEmulator(output_mode='voxel_grid') state machine, numpy float32."""
+    """EventEmulator state machine, numpy float32: output_mode 'voxel_grid' (default) or 'raw'."""
 
     def __init__(self, num_bins=5, pl=1.0, ps=1.0, ql=1.0, qs=1.0, pos_thres=0.2, neg_thres=0.2, sigma_thres=0.03,
                  cutoff_hz=0.0, leak_rate_hz=0.1, refractory_period_s=0.0, shot_noise_rate_hz=0.0,
-                 leak_jitter_fraction=0.1, noise_rate_cov_decades=0.1, rng=None):
+                 leak_jitter_fraction=0.1, noise_rate_cov_decades=0.1, rng=None, output_mode="voxel_grid"):
+        self.raw = output_mode == "raw"
         self.nb = num_bins
         self.pl, self.ps, self.ql, self.qs = pl, ps, ql, qs
         self.pos_nom, self.neg_nom = f32(pos_thres), f32(neg_thres)
@@ -212,7 +213,11 @@ class V2EOracle:
 
     def forward(self, frames, t_frames):
         """frames (B, F, H, W) float32 intensities 0..255; t_frames (B, 2) or (B, F) seconds.
-        Returns (voxels (B, nb, H, W) float32 before event_preprocess, num_events)."""
+        Returns (voxels (B, nb, H, W) float32 before event_preprocess, num_events), or in raw mode
+        (rows (N, 5) float32 [t, x, y, p, b], num_events): v2e_model.py:504-518 stacks each
+        iteration's events in nonzero (b, y, x) order and :527-534 sorts by t, then by b -- here
+        stable sorts (the reference's torch.sort makes no tie promise), so rows of equal (b, t)
+        keep their emission order."""
         frames = frames.astype(f32)
         B, F, H, W = frames.shape
         t_frames = np.asarray(t_frames, dtype=np.float64)
@@ -246,6 +251,8 @@ class V2EOracle:
         if not tf[1] > self.t_prev:
             raise ValueError("this frame time must be later than previous frame time")
         vox = np.zeros((B, nb, H, W), f32)
+        rows = []
+        loops = 0
         num_events = 0
         for n in range(1, F):
             new = filt[n]
@@ -282,6 +289,7 @@ class V2EOracle:
                 shot_cord = shot_on * (pol > 0) + shot_off * (pol < 0)
             final = np.zeros((B, 1, H, W), np.int32)
             refr_on = bool((Tr > ts_step[None, :]).any())        # (B, 1) > (B,) broadcasts, :447
+            loops += max_iters
             for i in range(max_iters):
                 mask = counts >= i + 1
                 if self.shot > 0:
@@ -293,6 +301,12 @@ class V2EOracle:
                     self.tmem[mask] = tsi[mask]
                 final += mask
                 t = (tsi * mask).astype(f32)
+                if self.raw:                                       # :505-518
+                    bb, _, yy, xx = np.nonzero(mask)
+                    num_events += len(bb)
+                    rows.append(np.stack([t[mask], xx.astype(f32), yy.astype(f32), pol[mask],
+                                          bb.astype(f32)], 1).astype(f32))
+                    continue
                 ti = np.floor(t)
                 dts = (t - ti).astype(f32)
                 vl = (pol * (f32(1) - dts)).astype(f32)
@@ -307,6 +321,13 @@ class V2EOracle:
                 np.add.at(vox, (bb, ti[tm2].astype(np.int64) + 1, yy, xx), vr[tm2])
             self.t_prev = tf[n]
             self.base = (self.base + pol * final.astype(f32) * C).astype(f32)
+        if self.raw:
+            if loops == 0:                                         # torch.tensor([]) (:347)
+                return np.zeros(0, f32), 0
+            ev = np.concatenate(rows, 0) if rows else np.zeros((0, 5), f32)
+            ev = ev[np.argsort(ev[:, 0], kind="stable")]           # :530-531
+            ev = ev[np.argsort(ev[:, 4], kind="stable")]           # :533-534
+            return ev, num_events
         return vox, num_events
 
 

@@ -180,3 +180,71 @@ def test_v2e2v_720x1280_two_packs_against_oracles():
             r, ref_states = ref_net.forward(torch.from_numpy(vox), torch.from_numpy(ref_prev), ref_states)
             ref_prev = r.numpy()
             assert rel_err(pred.cpu().numpy(), ref_prev) < 1e-4
+
+
+def run_raw_both(cfg, B=1, F=10, H=48, W=64, calls=2, cols=None, speeds=None):
+    emu = v2e.EventEmulator("raw", device="cuda", seed=5, **cfg)
+    ora = vo.V2EOracle(output_mode="raw", **cfg)
+    res = []
+    for k in range(calls):
+        fr = video(B, F, H, W, seed=1, t0=k, speed=1.5 if speeds is None else speeds[k])
+        tf = times(B, F, 0.1 * k + (k * 0.0001), cols=cols)
+        if k > 0:
+            tf = tf + (F - 1) * 0.01 * k
+        ev, n = emu(torch.from_numpy(fr).cuda(), torch.from_numpy(tf))
+        rv, rn = ora.forward(fr, tf)
+        res.append((ev.cpu().numpy(), n, rv, rn))
+    return res
+
+
+@pytest.mark.parametrize("extra", [{}, {"cutoff_hz": 30.0, "refractory_period_s": 0.004},
+                                   {"pos_thres": 0.015, "neg_thres": 0.015}])
+def test_raw_events_match_restatement(extra):
+    """output_mode='raw' (v2e_model.py:504-518,527-534): every row [t, x, y, p, b] bit-identical
+    to the numpy restatement's, in its order (b, then t, then pixel order).  pos/neg_thres 0.015
+    puts 32-47 iterations in most frame steps: two 32-iteration blocks."""
+    for ev, n, ref, rn in run_raw_both(dict(DET, **extra)):
+        assert n == rn > 0 and ev.shape == ref.shape == (n, 5)
+        np.testing.assert_array_equal(ev, ref)
+
+
+def test_raw_batch_two_column_times_and_buffer_regrowth():
+    """B=3 with (B, 2) timestamps; the second call has several times the first's events, so the
+    row buffer is too small: the library reports the count with the state untouched and the call
+    is replayed (a wrong restore would shift every later row)."""
+    res = run_raw_both(dict(DET, refractory_period_s=0.003), B=3, F=6, cols=True, calls=3, speeds=[0.2, 6.0, 6.0])
+    assert res[1][1] > 2 * res[0][1]
+    for ev, n, ref, rn in res:
+        assert n == rn
+        np.testing.assert_array_equal(ev, ref)
+
+
+def test_raw_random_configuration_matches_voxel_mode():
+    """Same seed, same random stream: the raw list holds exactly the voxel mode's events."""
+    cfg = dict(sigma_thres=0.03, leak_rate_hz=0.1, shot_noise_rate_hz=1.0, cutoff_hz=20.0, refractory_period_s=0.001)
+    fr = torch.from_numpy(video(2, 10, 64, 80, seed=3)).cuda()
+    tf = torch.from_numpy(times(2, 10, 0.0))
+    raw = [v2e.EventEmulator("raw", device="cuda", seed=11, **cfg)(fr, tf) for _ in range(2)]
+    _, n_vox = v2e.EventEmulator("voxel_grid", device="cuda", seed=11, **cfg)(fr, tf)
+    assert raw[0][1] == raw[1][1] == n_vox > 0 and torch.equal(raw[0][0], raw[1][0])
+    ev = raw[0][0].cpu().numpy()
+    key = np.lexsort((ev[:, 1], ev[:, 2], ev[:, 0], ev[:, 4]))
+    assert np.array_equal(key, np.arange(len(ev)))
+
+
+def test_raw_static_video_returns_1d_empty():
+    e = v2e.EventEmulator("raw", device="cuda", seed=2, **DET)
+    ev, n = e(torch.full((1, 4, 16, 16), 90.0, device="cuda"), torch.from_numpy(times(1, 4, 0.0)))
+    assert n == 0 and ev.shape == (0,) and ev.dtype == torch.float32
+
+
+def test_raw_720x1280_against_restatement():
+    """Config c5's frame size: 14 400 waves per element in the per-block offset scan."""
+    det = dict(DET, cutoff_hz=30.0, refractory_period_s=0.001)
+    H, W, F = 720, 1280, 10
+    fr = video(1, F, H, W, seed=4, speed=9.0)
+    tf = times(1, F, 0.0, dt=1.0 / 240.0)
+    ev, n = v2e.EventEmulator("raw", device="cuda", seed=3, **det)(torch.from_numpy(fr).cuda(), torch.from_numpy(tf))
+    ref, rn = vo.V2EOracle(output_mode="raw", **det).forward(fr, tf)
+    assert n == rn > 1000
+    np.testing.assert_array_equal(ev.cpu().numpy(), ref)

@@ -126,6 +126,10 @@ def _declare(lib):
         "cista_v2e_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
         "cista_v2e_forward": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int,
                                       c_int, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+        "cista_v2e_raw_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
+        "cista_v2e_forward_raw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_int,
+                                          c_int, c_int, c_void_p, ctypes.c_ulonglong, c_void_p, c_void_p, c_void_p,
+                                          c_size_t, c_void_p]),
     }
     for name, (res, args) in sig.items():
         fn = getattr(lib, name)

@@ -239,6 +239,63 @@ __global__ void v2e_iters_kernel(Call c, Scratch w) {
     w.meta[1] = refr;
 }
 
+// One pixel's event iterations of a frame step (v2e_model.py:449-473 with the shot noise of
+// emulator_utils.py:159-207): fire(it, ts) says whether iteration `it` emits an event and at
+// which voxel time.  Shared by the voxel-grid and the raw-event emission.
+struct PixelSteps {
+    int cnt, ni, B, b, HW, p, q_have;
+    float pol, on_thr, off_thr, step, Tr, t0, tmem;
+    bool shot, refr;
+    unsigned long long seed, dkey;
+    U4 rq;                                             // the 4 uniforms of iterations 4q .. 4q+3
+
+    __device__ __forceinline__ bool fire(int it, float &ts) {
+        bool m = cnt >= it + 1;                        // :459
+        // num_iter_mask (:196-198); the draw only matters when the count has not already set the
+        // mask (mask = count OR shot).  One Philox block serves 4 iterations.
+        if (shot && it < ni && !m) {
+            const int q = it >> 2;
+            if (q != q_have) {
+                rq = draw(seed, dkey, ((unsigned long long)q * B + b) * HW + p);
+                q_have = q;
+            }
+            const unsigned u = (it & 3) == 0 ? rq.x : (it & 3) == 1 ? rq.y : (it & 3) == 2 ? rq.z : rq.w;
+            const float r = u01(u);
+            m = pol > 0.0f ? r > on_thr : r < off_thr;
+        }
+        ts = it < ni ? t0 + step * (float)(it + 1) : 0.0f;   // :428-432
+        if (refr) {                                    // :469-473
+            const float since = ts * (m ? 1.0f : 0.0f) - tmem;
+            m = since > Tr;
+            if (m) tmem = ts;
+        }
+        return m;
+    }
+};
+
+__device__ __forceinline__ PixelSteps pixel_steps(const Call &c, const Scratch &w, int n, float dt_frame, int b, int p,
+                                                  int cnt, float pol, float fr, float pos_pre, float neg_pre,
+                                                  float tmem0) {
+    const cista_v2e_config &g = c.cfg;
+    PixelSteps q;
+    q.cnt = cnt; q.ni = w.num_iters[b]; q.B = c.B; q.b = b; q.HW = c.H * c.W; q.p = p; q.q_have = -1;
+    q.pol = pol; q.step = w.ts_step[b]; q.Tr = c.Tr[b]; q.t0 = c.time_frames[n - 1]; q.tmem = tmem0;
+    q.shot = g.shot_noise_rate_hz > 0.0f;
+    q.refr = w.meta[1] != 0;
+    q.seed = c.seed;
+    q.dkey = c.draw0 + 9 + 2 * (unsigned long long)n;
+    q.rq = U4{0u, 0u, 0u, 0u};
+    q.on_thr = 1.0f;
+    q.off_thr = 0.0f;
+    if (q.shot) {                                      // generate_shot_noise thresholds
+        const float inten = rescale(fr);
+        const float factor = (g.shot_noise_rate_hz / 2.0f * dt_frame / (float)q.ni) * ((0.25f - 1.0f) * inten + 1.0f);
+        q.on_thr = 1.0f - factor * pos_pre;
+        q.off_thr = factor * neg_pre;
+    }
+    return q;
+}
+
 // The voxel cells of a pixel are touched by this thread only, so they are loaded once (at the
 // pixel's first event) and accumulated in registers, in the reference's order -- bit-identical
 // to a read-modify-write per event (a cell never holds -0, so the +0 of the untouched cells'
@@ -264,49 +321,15 @@ __global__ __launch_bounds__(256) void v2e_emit_kernel(Call c, State s, Scratch 
         int final_cnt = 0;
         if (pol != 0.0f) {                 // pol == 0: no count, no shot noise, no event (exact skip)
             const int max_iters = w.meta[0];
-            const bool refr = w.meta[1] != 0;
-            const int ni = w.num_iters[b];
-            const float step = w.ts_step[b];
-            const float Tr = c.Tr[b];
+            PixelSteps px = pixel_steps(c, w, n, dt_frame, b, p, cnt, pol, fr, pos_pre, neg_pre, tmem0);
             const int nb = c.nb;
-            // shot noise thresholds (generate_shot_noise, emulator_utils.py:159-207)
-            float on_thr = 1.0f, off_thr = 0.0f;
-            if (shot) {
-                const float inten = rescale(fr);
-                const float factor = (g.shot_noise_rate_hz / 2.0f * dt_frame / (float)ni) * ((0.25f - 1.0f) * inten + 1.0f);
-                on_thr = 1.0f - factor * pos_pre;
-                off_thr = factor * neg_pre;
-            }
-            float tmem = tmem0;
             float *vp = vox + (size_t)b * nb * HW + p;
-            const float t0 = c.time_frames[n - 1];
             float cell[NB];
             unsigned touched = 0;
             bool loaded = false;
-            U4 rq{0u, 0u, 0u, 0u};                         // the 4 uniforms of iterations 4q .. 4q+3
-            int q_have = -1;
             for (int it = 0; it < max_iters; ++it) {
-                bool m = cnt >= it + 1;                        // :459
-                // num_iter_mask (:196-198); the draw only matters when the count has not already
-                // set the mask (mask = count OR shot).  One Philox block serves 4 iterations.
-                if (shot && it < ni && !m) {
-                    const int q = it >> 2;
-                    if (q != q_have) {
-                        rq = draw(c.seed, c.draw0 + 9 + 2 * (unsigned long long)n,
-                                  ((unsigned long long)q * c.B + b) * HW + p);
-                        q_have = q;
-                    }
-                    const unsigned u = (it & 3) == 0 ? rq.x : (it & 3) == 1 ? rq.y : (it & 3) == 2 ? rq.z : rq.w;
-                    const float r = u01(u);
-                    m = pol > 0.0f ? r > on_thr : r < off_thr;
-                }
-                const float ts = it < ni ? t0 + step * (float)(it + 1) : 0.0f;   // :428-432
-                if (refr) {                                    // :469-473
-                    const float since = ts * (m ? 1.0f : 0.0f) - tmem;
-                    m = since > Tr;
-                    if (m) tmem = ts;
-                }
-                if (!m) continue;
+                float ts;
+                if (!px.fire(it, ts)) continue;
                 final_cnt += 1;                                // :476
                 const float ti = floorf(ts);                   // :479-484
                 const float dts = ts - ti;
@@ -332,7 +355,7 @@ __global__ __launch_bounds__(256) void v2e_emit_kernel(Call c, State s, Scratch 
 #pragma unroll
             for (int j = 0; j < NB; ++j)
                 if ((touched >> j) & 1u) vp[(size_t)j * HW] = cell[j];
-            if (refr) s.tmem[i] = tmem;
+            if (px.refr) s.tmem[i] = px.tmem;
         }
         s.base[i] = base + pol * (float)final_cnt * C;        // :520
     }
@@ -354,6 +377,157 @@ __global__ void v2e_nev_kernel(Scratch w, unsigned long long *out) {
     unsigned long long t = w.nev[threadIdx.x * (SLOTW / 2)];   // 64 lanes = MAXSLOTS slots
     for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
     if (threadIdx.x == 0) *out = t;
+}
+
+// ------------------------------------------------------------------ raw-event mode
+// output_mode='raw' (v2e_model.py:504-518,527-534): rows [t, x, y, p, b] (float32) of every
+// event, sorted by batch element, then timestamp.  Within one element the timestamps grow with
+// (frame n, iteration it) -- every event has it < num_iters[b], so t = time_frames[n-1] +
+// ts_step * (it + 1) > 0 -- and the rows of one (b, n, it) share t, kept in the reference's
+// emission order (y, x): the row order is (b, n, it, y, x), the result of the reference's two
+// sorts when ties keep their emission order.  Rows are written in place, no sort: a count pass
+// over the whole call gives every element's row range, then the call is replayed from the same
+// state and random stream, each iteration block of 32 writing its rows at offsets from an
+// exclusive scan of per-wave event counts.
+struct RawScratch {
+    float *snap;                   // base, lp, tmem planes at the start of the call
+    unsigned *bits;                // B*HW: fired iterations of the current 32-iteration block
+    unsigned *cnt;                 // [B][32][nchunks] per-wave event counts, then their first rows
+    unsigned long long *totb;      // [B][MAXSLOTS][SLOTW/2] partial event totals per element
+    unsigned long long *run;       // [B] next output row of each element, [B] the call's total
+    int *mis;                      // [CISTA_V2E_MAX_FRAMES] max_num_iters of each frame step
+    int nchunks;                   // 64-pixel waves per batch element
+};
+
+// One wave = 64 consecutive pixels of one element (grid (ceil(nchunks / 4), B)).  COUNT: the
+// frame step with its state update, adding the events to the element's total.  Otherwise the
+// step replayed for iterations [32 blk, 32 blk + 32): fired-iteration bits per pixel and event
+// counts per (iteration, wave); `update` (the last block) also writes base / tmem.
+template <bool COUNT>
+__global__ __launch_bounds__(256) void v2e_raw_emit_kernel(Call c, State s, Scratch w, RawScratch r,
+                                                           const float *frames, int n, float dt_frame, int blk,
+                                                           int update) {
+    const int HW = c.H * c.W;
+    const int b = blockIdx.y, chunk = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int p = chunk * 64 + lane;
+    const int i = b * HW + p;
+    unsigned bits = 0, nev = 0;
+    if (p < HW) {
+        const bool shot = c.cfg.shot_noise_rate_hz > 0.0f;
+        const int cnt = w.counts[i];
+        const float pol = w.pol[i];
+        const float pos = s.pos[i], neg = s.neg[i], base = s.base[i], tmem0 = s.tmem[i];
+        const float fr = shot ? frames[((size_t)b * c.F + n) * HW + p] : 0.0f;
+        const float pos_pre = shot ? s.pos_pre[i] : 0.0f, neg_pre = shot ? s.neg_pre[i] : 0.0f;
+        const float C = (pol > 0.0f ? pos : 0.0f) + (pol < 0.0f ? neg : 0.0f);
+        int final_cnt = 0;
+        if (pol != 0.0f) {
+            const int max_iters = w.meta[0];
+            const int lo = 32 * blk;
+            const int end = update ? max_iters : min(max_iters, lo + 32);
+            PixelSteps px = pixel_steps(c, w, n, dt_frame, b, p, cnt, pol, fr, pos_pre, neg_pre, tmem0);
+            for (int it = 0; it < end; ++it) {
+                float ts;
+                if (!px.fire(it, ts)) continue;
+                final_cnt += 1;
+                if (it >= lo && it < lo + 32) bits |= 1u << (it - lo);
+            }
+            if (update && px.refr) s.tmem[i] = px.tmem;
+        }
+        if (update) s.base[i] = base + pol * (float)final_cnt * C;   // :520
+        nev = (unsigned)final_cnt;
+    }
+    if (COUNT) {
+        unsigned t = nev;
+        for (int o = 32; o > 0; o >>= 1) t += __shfl_xor(t, o);
+        if (lane == 0 && t != 0u)
+            atomicAdd(r.totb + ((size_t)b * MAXSLOTS + chunk % MAXSLOTS) * (SLOTW / 2), (unsigned long long)t);
+    } else {
+        if (p < HW) r.bits[i] = bits;
+        unsigned mine = 0;
+        for (int j = 0; j < 32; ++j) {
+            const unsigned cj = (unsigned)__popcll(__ballot((bits >> j) & 1u));
+            if (lane == j) mine = cj;
+        }
+        if (lane < 32 && chunk < r.nchunks) r.cnt[((size_t)b * 32 + lane) * r.nchunks + chunk] = mine;
+    }
+}
+
+// Row ranges of the elements from the count pass: run[b] = rows of elements < b, run[B] = total.
+__global__ void v2e_raw_offsets_kernel(RawScratch r, int B) {
+    if (threadIdx.x != 0) return;
+    unsigned long long acc = 0;
+    for (int b = 0; b < B; ++b) {
+        unsigned long long t = 0;
+        for (int k = 0; k < MAXSLOTS; ++k) t += r.totb[((size_t)b * MAXSLOTS + k) * (SLOTW / 2)];
+        r.run[b] = acc;
+        acc += t;
+    }
+    r.run[B] = acc;
+}
+
+// One workgroup per element: the counts [32][nchunks] (iteration-major, then pixel order) become
+// exclusive row offsets starting at run[b], which then moves past this block's rows.
+__global__ __launch_bounds__(1024) void v2e_raw_scan_kernel(RawScratch r) {
+    __shared__ unsigned wsum[16];
+    const int b = blockIdx.x;
+    const int n = 32 * r.nchunks;
+    unsigned *a = r.cnt + (size_t)b * n;
+    const int per = (n + 1023) / 1024;
+    const int lo = min(n, (int)threadIdx.x * per), hi = min(n, lo + per);
+    const unsigned long long start = r.run[b];       // read before the barrier, written after
+    unsigned sum = 0;
+    for (int k = lo; k < hi; ++k) sum += a[k];
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned v = sum;                                 // inclusive scan within the wave
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(v, o);
+        if (lane >= o) v += t;
+    }
+    if (lane == 63) wsum[wv] = v;
+    __syncthreads();
+    unsigned before = 0;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
+    unsigned pos = (unsigned)start + before + v - sum;
+    for (int k = lo; k < hi; ++k) {
+        const unsigned x = a[k];
+        a[k] = pos;
+        pos += x;
+    }
+    if (threadIdx.x == 1023) r.run[b] = start + before + v;
+}
+
+// The rows of iteration block `blk`: an event's row is its (iteration, wave) offset plus its rank
+// among the wave's lanes firing at that iteration (pixel order).
+__global__ __launch_bounds__(256) void v2e_raw_fill_kernel(Call c, Scratch w, RawScratch r, int n, int blk,
+                                                           float *events, unsigned long long capacity) {
+    const int HW = c.H * c.W;
+    const int b = blockIdx.y, chunk = blockIdx.x * 4 + (int)(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (chunk >= r.nchunks) return;                   // whole waves
+    const int p = chunk * 64 + lane;
+    const unsigned bits = p < HW ? r.bits[b * HW + p] : 0u;
+    if (__ballot(bits != 0u) == 0ull) return;
+    const float step = w.ts_step[b], t0 = c.time_frames[n - 1];
+    const float pol = p < HW ? w.pol[b * HW + p] : 0.0f;
+    const int y = p / c.W, x = p - y * c.W;
+    const unsigned *off = r.cnt + (size_t)b * 32 * r.nchunks + chunk;
+    const unsigned long long below = (1ull << lane) - 1ull;
+    for (int j = 0; j < 32; ++j) {
+        const bool m = (bits >> j) & 1u;
+        const unsigned long long bal = __ballot(m);
+        if (bal == 0ull) continue;
+        if (m) {
+            const unsigned long long row = (unsigned long long)off[(size_t)j * r.nchunks] + __popcll(bal & below);
+            if (row < capacity) {
+                float *e = events + row * 5;
+                e[0] = t0 + step * (float)(32 * blk + j + 1);   // the PixelSteps::fire timestamp
+                e[1] = (float)x;
+                e[2] = (float)y;
+                e[3] = pol;
+                e[4] = (float)b;
+            }
+        }
+    }
 }
 
 inline size_t align_up(size_t x) { return (x + 255) & ~(size_t)255; }
@@ -419,36 +593,34 @@ void linspace_f32(float start, float end, int steps, float *out) {
         out[k] = k < halfway ? start + step * (float)k : end - step * (float)(steps - k - 1);
 }
 
-}  // namespace cista_v2e
-
-using namespace cista_v2e;
-
-extern "C" {
-
-size_t cista_v2e_state_bytes(int B, int H, int W) {
-    if (B <= 0 || H <= 0 || W <= 0) return 0;
-    return state_bytes(B, H, W);
+RawScratch carve_raw(void *base, int B, int H, int W, size_t *bytes) {
+    RawScratch r;
+    size_t off = 0;
+    const size_t n = (size_t)B * H * W;
+    char *p = static_cast<char *>(base);
+    auto take = [&](size_t nbytes) {
+        void *q = p ? p + off : nullptr;
+        off = align_up(off + nbytes);
+        return q;
+    };
+    r.nchunks = (H * W + 63) / 64;
+    r.snap = static_cast<float *>(take(3 * n * 4));
+    r.bits = static_cast<unsigned *>(take(n * 4));
+    r.cnt = static_cast<unsigned *>(take((size_t)B * 32 * r.nchunks * 4));
+    r.totb = static_cast<unsigned long long *>(take((size_t)B * MAXSLOTS * (SLOTW / 2) * 8));
+    r.run = static_cast<unsigned long long *>(take(((size_t)B + 1) * 8));
+    r.mis = static_cast<int *>(take(CISTA_V2E_MAX_FRAMES * 4));
+    *bytes = off;
+    return r;
 }
 
-size_t cista_v2e_workspace_bytes(int B, int H, int W) {
-    if (B <= 0 || H <= 0 || W <= 0) return 0;
-    return carve_ws(nullptr, B, H, W, 16).bytes;   // sized for up to 16 bins
-}
-
-int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, void *state, const float *frames,
-                      const double *t_frames, int t_cols, int B, int F, int H, int W, float *voxels,
-                      unsigned long long *num_events, void *workspace, size_t workspace_bytes, void *stream) {
-    if (!cfg || !hs || !state || !frames || !t_frames || !voxels || !workspace) return CISTA_ERR_INVALID;
+// The per-call constants (v2e_model.py:303-322 and the low-pass time constants :266-289).
+int make_call(const cista_v2e_config *cfg, const double *t_frames, int t_cols, int B, int F, int H, int W, Call &c) {
     if (B <= 0 || B > CISTA_V2E_MAX_BATCH || F < 2 || F > CISTA_V2E_MAX_FRAMES || H <= 0 || W <= 0)
         return B > CISTA_V2E_MAX_BATCH || F > CISTA_V2E_MAX_FRAMES ? CISTA_ERR_UNSUPPORTED : CISTA_ERR_INVALID;
     if (cfg->num_bins < 2 || cfg->num_bins > 16 || (t_cols != 2 && t_cols != F)) return CISTA_ERR_INVALID;
-    const WsLayout L = carve_ws(workspace, B, H, W, cfg->num_bins);
-    if (workspace_bytes < L.bytes) return CISTA_ERR_WORKSPACE;
-    hipStream_t st = static_cast<hipStream_t>(stream);
-    const State s = carve_state(state, B, H, W);
+    if ((long long)B * H * W >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;        // 32-bit pixel index
     const int nb = cfg->num_bins;
-
-    Call c;
     memset(&c, 0, sizeof(c));
     c.B = B; c.F = F; c.H = H; c.W = W; c.nb = nb;
     c.cfg = *cfg;
@@ -473,25 +645,71 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
         }
     }
     c.linlog_f = (1.0 / 20.0) * log(20.0);
-    const long long npx = (long long)B * H * W;
-    if (npx >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;                          // 32-bit pixel index
+    return CISTA_OK;
+}
 
+// Start of a forward call: _init on the first call, else the refractory-memory shift (:324-331);
+// the frame-time check (:339-342); cleared event / image-max slots; this call's random stream.
+int begin_call(Call &c, const State &s, const Scratch &sc, cista_v2e_host_state *hs, const float *frames,
+               const double *t_frames, hipStream_t st) {
+    const long long npx = (long long)c.B * c.H * c.W;
     if (!hs->initialized) {
         c.draw0 = hs->draw;
         hipLaunchKernelGGL(v2e_init_kernel, g1d(npx), dim3(256), 0, st, c, s, frames);
         hs->draw += 8;
         hs->t_previous = (float)t_frames[0];
         hs->initialized = 1;
-    } else if (cfg->refractory_period_s > 0.0f) {
+    } else if (c.cfg.refractory_period_s > 0.0f) {
         hipLaunchKernelGGL(v2e_tmem_kernel, g1d(npx), dim3(256), 0, st, c, s);
     }
     if (!(c.tf[1] > hs->t_previous)) return CISTA_ERR_INVALID;                     // :339-342
-    if (hipMemsetAsync(voxels, 0, (size_t)B * nb * H * W * 4, st) != hipSuccess) return CISTA_ERR_HIP;
-    if (hipMemsetAsync(L.sc.nev, 0, MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+    if (hipMemsetAsync(sc.nev, 0, MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     c.draw0 = hs->draw;
-    hs->draw += 2 * (unsigned long long)F + 16;
+    hs->draw += 2 * (unsigned long long)c.F + 16;
     // the image-max slots start cleared; each frame's v2e_iters_kernel clears them after reading
-    if (hipMemsetAsync(L.sc.iters_raw, 0, (size_t)B * MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+    if (hipMemsetAsync(sc.iters_raw, 0, (size_t)c.B * MAXSLOTS * SLOTW * 4, st) != hipSuccess) return CISTA_ERR_HIP;
+    return CISTA_OK;
+}
+
+}  // namespace cista_v2e
+
+using namespace cista_v2e;
+
+extern "C" {
+
+size_t cista_v2e_state_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return state_bytes(B, H, W);
+}
+
+size_t cista_v2e_workspace_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    return carve_ws(nullptr, B, H, W, 16).bytes;   // sized for up to 16 bins
+}
+
+size_t cista_v2e_raw_workspace_bytes(int B, int H, int W) {
+    if (B <= 0 || H <= 0 || W <= 0) return 0;
+    size_t raw = 0;
+    carve_raw(nullptr, B, H, W, &raw);
+    return carve_ws(nullptr, B, H, W, 16).bytes + raw;
+}
+
+int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, void *state, const float *frames,
+                      const double *t_frames, int t_cols, int B, int F, int H, int W, float *voxels,
+                      unsigned long long *num_events, void *workspace, size_t workspace_bytes, void *stream) {
+    if (!cfg || !hs || !state || !frames || !t_frames || !voxels || !workspace) return CISTA_ERR_INVALID;
+    Call c;
+    const int rc = make_call(cfg, t_frames, t_cols, B, F, H, W, c);
+    if (rc != CISTA_OK) return rc;
+    const WsLayout L = carve_ws(workspace, B, H, W, cfg->num_bins);
+    if (workspace_bytes < L.bytes) return CISTA_ERR_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const State s = carve_state(state, B, H, W);
+    const int nb = cfg->num_bins;
+    const long long npx = (long long)B * H * W;
+    const int rb = begin_call(c, s, L.sc, hs, frames, t_frames, st);
+    if (rb != CISTA_OK) return rb;
+    if (hipMemsetAsync(voxels, 0, (size_t)B * nb * H * W * 4, st) != hipSuccess) return CISTA_ERR_HIP;
     for (int n = 1; n < F; ++n) {
         const float dt = c.tf[n] - hs->t_previous;                                 // :352
         hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
@@ -507,6 +725,97 @@ int cista_v2e_forward(const cista_v2e_config *cfg, cista_v2e_host_state *hs, voi
     // event_preprocess_pytorch(mode='std', filter_hot_pixel=False) over the whole tensor (:526)
     return cista_voxel_preprocess(voxels, 1, B * nb, H, W, CISTA_VOXEL_STD_F32, 0.0f, L.vox_ws, L.vox_ws_bytes,
                                   stream);
+}
+
+int cista_v2e_forward_raw(const cista_v2e_config *cfg, cista_v2e_host_state *hs, void *state, const float *frames,
+                          const double *t_frames, int t_cols, int B, int F, int H, int W, float *events,
+                          unsigned long long capacity, unsigned long long *num_events, int *loop_iterations,
+                          void *workspace, size_t workspace_bytes, void *stream) {
+    if (!cfg || !hs || !state || !frames || !t_frames || !num_events || !workspace || (capacity && !events))
+        return CISTA_ERR_INVALID;
+    Call c;
+    const int rc = make_call(cfg, t_frames, t_cols, B, F, H, W, c);
+    if (rc != CISTA_OK) return rc;
+    const WsLayout L = carve_ws(workspace, B, H, W, cfg->num_bins);
+    size_t raw_bytes = 0;
+    const RawScratch r = carve_raw(static_cast<char *>(workspace) + L.bytes, B, H, W, &raw_bytes);
+    if (workspace_bytes < L.bytes + raw_bytes) return CISTA_ERR_WORKSPACE;
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    const State s = carve_state(state, B, H, W);
+    const long long npx = (long long)B * H * W;
+    const size_t plane = (size_t)npx * 4;
+    const dim3 wgrid((unsigned)((r.nchunks + 3) / 4), (unsigned)B);
+    const cista_v2e_host_state hs0 = *hs;
+    // base / lp / tmem are the state a call changes once initialised (thresholds and noise rates
+    // are fixed at _init, which replays identically from the same random-stream counter)
+    if (hs0.initialized) {
+        if (hipMemcpyAsync(r.snap, s.base, plane, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(r.snap + npx, s.lp, plane, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(r.snap + 2 * npx, s.tmem, plane, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return CISTA_ERR_HIP;
+    }
+    auto restore = [&]() -> int {
+        *hs = hs0;
+        if (!hs0.initialized) return CISTA_OK;
+        if (hipMemcpyAsync(s.base, r.snap, plane, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(s.lp, r.snap + npx, plane, hipMemcpyDeviceToDevice, st) != hipSuccess ||
+            hipMemcpyAsync(s.tmem, r.snap + 2 * npx, plane, hipMemcpyDeviceToDevice, st) != hipSuccess)
+            return CISTA_ERR_HIP;
+        return CISTA_OK;
+    };
+
+    // pass 1: the call's frame steps, counting each element's events
+    int rb = begin_call(c, s, L.sc, hs, frames, t_frames, st);
+    if (rb != CISTA_OK) return rb;
+    if (hipMemsetAsync(r.totb, 0, (size_t)B * MAXSLOTS * (SLOTW / 2) * 8, st) != hipSuccess) return CISTA_ERR_HIP;
+    for (int n = 1; n < F; ++n) {
+        const float dt = c.tf[n] - hs->t_previous;
+        hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
+        hipLaunchKernelGGL(v2e_iters_kernel, dim3(1), dim3(64), 0, st, c, L.sc);
+        if (hipMemcpyAsync(r.mis + n, L.sc.meta, 4, hipMemcpyDeviceToDevice, st) != hipSuccess) return CISTA_ERR_HIP;
+        hipLaunchKernelGGL(v2e_raw_emit_kernel<true>, wgrid, dim3(256), 0, st, c, s, L.sc, r, frames, n, dt, 0, 1);
+        hs->t_previous = c.tf[n];
+    }
+    hipLaunchKernelGGL(v2e_raw_offsets_kernel, dim3(1), dim3(64), 0, st, r, B);
+    if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
+    unsigned long long total = 0;
+    int mis[CISTA_V2E_MAX_FRAMES] = {0};
+    if (hipMemcpyAsync(&total, r.run + B, 8, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipMemcpyAsync(mis + 1, r.mis + 1, (size_t)(F - 1) * 4, hipMemcpyDeviceToHost, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess)
+        return CISTA_ERR_HIP;
+    *num_events = total;
+    if (loop_iterations) {
+        int sum = 0;
+        for (int n = 1; n < F; ++n) sum += mis[n];
+        *loop_iterations = sum;
+    }
+    if (total > capacity || total >= (1ull << 32)) {   // the caller sizes `events` and calls again
+        const int rr = restore();
+        if (rr != CISTA_OK) return rr;
+        return total >= (1ull << 32) ? CISTA_ERR_UNSUPPORTED : CISTA_ERR_WORKSPACE;
+    }
+
+    // pass 2: the same steps from the same state and random stream, writing the rows
+    rb = restore();
+    if (rb != CISTA_OK) return rb;
+    rb = begin_call(c, s, L.sc, hs, frames, t_frames, st);
+    if (rb != CISTA_OK) return rb;
+    for (int n = 1; n < F; ++n) {
+        const float dt = c.tf[n] - hs->t_previous;
+        hipLaunchKernelGGL(v2e_diff_kernel, g1d(npx), dim3(256), 0, st, c, s, L.sc, frames, n, dt);
+        hipLaunchKernelGGL(v2e_iters_kernel, dim3(1), dim3(64), 0, st, c, L.sc);
+        const int nblk = mis[n] > 0 ? (mis[n] + 31) / 32 : 1;
+        for (int blk = 0; blk < nblk; ++blk) {
+            hipLaunchKernelGGL(v2e_raw_emit_kernel<false>, wgrid, dim3(256), 0, st, c, s, L.sc, r, frames, n, dt, blk,
+                               blk == nblk - 1 ? 1 : 0);
+            if (mis[n] == 0) continue;
+            hipLaunchKernelGGL(v2e_raw_scan_kernel, dim3((unsigned)B), dim3(1024), 0, st, r);
+            hipLaunchKernelGGL(v2e_raw_fill_kernel, wgrid, dim3(256), 0, st, c, L.sc, r, n, blk, events, capacity);
+        }
+        hs->t_previous = c.tf[n];
+    }
+    return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
 
 }  // extern "C"

@@ -1,15 +1,17 @@
 """Video-to-events emulator and the V2E2V pipeline on the GPU.
 
 ``EventEmulator`` mirrors reference v2e/v2e_model.py:31-536 (same constructor arguments and
-defaults, ``reset()``, ``forward(frames, t_frames) -> (events, num_events)``) for
-``output_mode='voxel_grid'``, the mode V2E2VNet uses (model_v2e2v.py:28-29,46-61); the whole
-frame step runs in libcista_hip.so (include/cista_v2e.h).  ``V2E2VNet`` mirrors
-model_v2e2v.py:9-128: emulator + the drop-in CistaLSTCNet.
+defaults, ``reset()``, ``forward(frames, t_frames) -> (events, num_events)``) in both output
+modes: ``'voxel_grid'``, the mode V2E2VNet uses (model_v2e2v.py:28-29,46-61), and ``'raw'``, the
+sorted [t, x, y, p, b] event list (:504-518,527-534); the whole frame step runs in
+libcista_hip.so (include/cista_v2e.h).  ``V2E2VNet`` mirrors model_v2e2v.py:9-128: emulator + the
+drop-in CistaLSTCNet.
 
 Differences, by design: random draws come from a counter-based Philox stream keyed by ``seed``
 (statistically the reference's torch.normal / randn / rand, not the same numbers); ``seed=0``
-draws a fresh seed like the reference's unseeded torch RNG.  The raw-event output mode and the
-cv2 state display are not built (V2E2V never uses them).
+draws a fresh seed like the reference's unseeded torch RNG.  Raw rows of equal (b, t) keep their
+emission order (y, x), which the reference's unstable torch.sort does not promise.  The cv2
+state display is not built (V2E2V never uses it).
 """
 from __future__ import annotations
 
@@ -157,8 +159,8 @@ class EventEmulator(torch.nn.Module):
                  leak_jitter_fraction=0.1, noise_rate_cov_decades=0.1, seed=0, show_dvs_model_state=None,
                  device="cuda", lazy_count=False):
         super().__init__()
-        if output_mode != "voxel_grid":
-            raise NotImplementedError("only output_mode='voxel_grid' (the V2E2V mode) is built")
+        if output_mode not in ("voxel_grid", "raw"):
+            raise ValueError(f"output_mode must be 'voxel_grid' or 'raw', not {output_mode!r}")
         if show_dvs_model_state:
             raise NotImplementedError("the cv2 model-state display is not built")
         self.output_mode = output_mode
@@ -173,6 +175,8 @@ class EventEmulator(torch.nn.Module):
         self.frame_counter = 0
         self._shape = None
         self.lazy_count = lazy_count   # True: num_events is an EventCount (no host sync per call)
+        self._rows = None              # raw mode: the event-row buffer, grown on demand
+        self.ws = None
 
     def reset(self):
         """v2e_model.py:255-263: the next forward re-initialises the base frame."""
@@ -181,7 +185,8 @@ class EventEmulator(torch.nn.Module):
 
     def forward(self, frames, t_frames):
         """frames (B, F, H, W) intensities 0..255; t_frames (B, 2) or (B, F) seconds.
-        Returns (voxels (B, num_bins, H, W), num_events)."""
+        Returns (voxels (B, num_bins, H, W), num_events) in voxel_grid mode, (events (N, 5) float32
+        rows [t, x, y, p, b], num_events) in raw mode (v2e_model.py:290-536)."""
         if not frames.is_cuda:
             raise _lib.CistaError("the event emulator runs on a ROCm GPU only (no CPU fallback)")
         B, F, H, W = frames.shape
@@ -191,23 +196,55 @@ class EventEmulator(torch.nn.Module):
         if tf.ndim != 2 or tf.shape[0] != B or tf.shape[1] not in (2, F):
             raise ValueError("t_frames must be (batch, 2) or (batch, num_frames)")
         L = _lib.lib()
+        raw = self.output_mode == "raw"
         if self.state is None or self._shape != (B, H, W) or self.state.device != fr.device:
             self.state = torch.empty(L.cista_v2e_state_bytes(B, H, W), dtype=torch.uint8, device=fr.device)
-            self.ws = torch.empty(L.cista_v2e_workspace_bytes(B, H, W), dtype=torch.uint8, device=fr.device)
             self._shape = (B, H, W)
+            self.ws = None
             self.hs.initialized = 0
+        if self.ws is None:
+            nbytes = (L.cista_v2e_raw_workspace_bytes if raw else L.cista_v2e_workspace_bytes)(B, H, W)
+            self.ws = torch.empty(nbytes, dtype=torch.uint8, device=fr.device)
+        stream = _lib.stream_handle(fr.device)
+        if raw:
+            return self._forward_raw(L, fr, tf, B, F, H, W, stream)
         out = torch.empty(B, self.num_bins, H, W, device=fr.device)
         nev = torch.zeros(1, dtype=torch.int64, device=fr.device)
         status = L.cista_v2e_forward(ctypes.byref(self.cfg), ctypes.byref(self.hs), self.state.data_ptr(),
                                      fr.data_ptr(), tf.ctypes.data, tf.shape[1], B, F, H, W, out.data_ptr(),
-                                     nev.data_ptr(), self.ws.data_ptr(), self.ws.numel(),
-                                     _lib.stream_handle(fr.device))
-        if status == 1 and self.hs.initialized:
-            raise ValueError("this frame time must be later than previous frame time")   # :339-342
-        _lib.check(status, "cista_v2e_forward")
+                                     nev.data_ptr(), self.ws.data_ptr(), self.ws.numel(), stream)
+        self._check_status(status, "cista_v2e_forward")
         # the reference returns a Python int; lazy_count keeps it on the device until it is read
         self.num_events = EventCount(nev) if self.lazy_count else int(nev.item())
         return out, self.num_events
+
+    def _check_status(self, status, what):
+        if status == 1 and self.hs.initialized:
+            raise ValueError("this frame time must be later than previous frame time")   # :339-342
+        _lib.check(status, what)
+
+    def _forward_raw(self, L, fr, tf, B, F, H, W, stream):
+        """Raw rows [t, x, y, p, b] sorted by b then t (:527-534); t in voxel-time units as the
+        reference emits them.  The library reports the event count first when the row buffer is
+        too small (the emulator state untouched), so the buffer grows and the call repeats once."""
+        n = ctypes.c_ulonglong(0)
+        loops = ctypes.c_int(0)
+        for attempt in range(2):
+            cap = 0 if self._rows is None else self._rows.shape[0]
+            status = L.cista_v2e_forward_raw(ctypes.byref(self.cfg), ctypes.byref(self.hs), self.state.data_ptr(),
+                                             fr.data_ptr(), tf.ctypes.data, tf.shape[1], B, F, H, W,
+                                             None if self._rows is None else self._rows.data_ptr(), cap,
+                                             ctypes.byref(n), ctypes.byref(loops), self.ws.data_ptr(),
+                                             self.ws.numel(), stream)
+            if status == 4 and attempt == 0:          # CISTA_ERR_WORKSPACE: rows needed = n
+                self._rows = torch.empty(max(int(n.value), 2 * cap), 5, dtype=torch.float32, device=fr.device)
+                continue
+            self._check_status(status, "cista_v2e_forward_raw")
+            break
+        self.num_events = int(n.value)
+        if loops.value == 0:                          # no iteration ran: torch.tensor([]) (:347)
+            return torch.zeros(0, device=fr.device), self.num_events
+        return self._rows[:self.num_events].clone(), self.num_events
 
 
 class V2E2VNet(torch.nn.Module):
