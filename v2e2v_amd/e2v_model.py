@@ -19,6 +19,7 @@ Differences a caller can observe (all documented in DESIGN.md):
 from __future__ import annotations
 
 import ctypes
+import weakref
 
 import torch
 import torch.nn as nn
@@ -52,6 +53,7 @@ class CistaLSTCNet(nn.Module):
         self._packed = None
         self._packed_key = None
         self._ws = None
+        self._conduit = None
 
     # ------------------------------------------------------------------ internals
     def _cfg(self):
@@ -97,12 +99,43 @@ class CistaLSTCNet(nn.Module):
         self._packed, self._packed_key = packed, key
         return packed
 
+    def _grad_conduit(self):
+        """One flat tensor, torch.cat of the unique parameters (each slot padded to 64 floats),
+        that every training frame takes as its parameter input.  Autograd then sums the frames'
+        parameter gradients as one flat add per frame (instead of one small add per parameter
+        and frame: 24 x 14 launches per BPTT step), and CatBackward hands each parameter its
+        slice once.  Rebuilt when a parameter changes, and dropped as soon as its gradient has
+        been computed, so the next sequence's frames start a fresh graph."""
+        params = self._unique_params()
+        key = tuple((p.data_ptr(), p._version, p.requires_grad) for p in params)
+        if self._conduit is not None and self._conduit[0] == key:
+            return self._conduit[1]
+        parts = []
+        for p in params:
+            parts.append(p.reshape(-1))
+            pad = -p.numel() % 64
+            if pad:
+                parts.append(p.new_zeros(pad))
+        flat = torch.cat(parts)
+        token = object()
+        if flat.requires_grad:
+            ref = weakref.ref(self)
+
+            def consumed(_grad):
+                m = ref()
+                if m is not None and m._conduit is not None and m._conduit[2] is token:
+                    m._conduit = None
+            flat.register_hook(consumed)
+        self._conduit = (key, flat, token)
+        return flat
+
     def invalidate_packed(self):
         """Drop the packed split-fp16 weights: the next forward repacks.  Needed after writing
         parameters through ``.data`` (e.g. ``Lambda.data.clamp_(min=0)``), which PyTorch does
         not version-count; load_state_dict and .to()/.cuda() invalidate automatically."""
         self._packed = None
         self._packed_key = None
+        self._conduit = None
 
     def _load_from_state_dict(self, *args, **kwargs):
         self.invalidate_packed()
@@ -222,7 +255,7 @@ def _cl(t):
 
 class _CistaFrame(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, model, events, prev_image, c_lstc_p, z_p, h_p, c_p, *params):
+    def forward(ctx, model, events, prev_image, c_lstc_p, z_p, h_p, c_p, flat_params):
         packed = model.packed_params()
         dev = packed.device
         B, nb, H, W = events.shape
@@ -273,13 +306,18 @@ class _CistaFrame(torch.autograd.Function):
         g_zp = torch.empty_like(zp, memory_format=torch.channels_last) if (zp is not None and need[4]) else None
         g_hp = torch.empty_like(hp, memory_format=torch.channels_last) if (hp is not None and need[5]) else None
         g_cp = torch.empty_like(cp, memory_format=torch.channels_last) if (cp is not None and need[6]) else None
-        pgrads = [torch.empty_like(p) for p in params]
+        # the gradient of the flat parameter conduit, each parameter at its padded slot
+        offs, n = [], 0
+        for p in params:
+            offs.append(n)
+            n += p.numel() + (-p.numel() % 64)
+        g_flat = torch.empty(n, device=dev)
         P = _lib.ptr
         io = _lib.CistaFrameIO(P(ev), P(pi), P(clp), P(zp), P(hp), P(cp), P(rec), P(c_lstc), P(z), P(hs), P(cs))
         gio = _lib.CistaGradIO(P(g_rec), P(g_cl), P(g_z), P(g_h), P(g_c), P(g_pi), P(g_clp), P(g_zp),
                                P(g_hp), P(g_cp), P(g_ev))
         cp_ = _lib.CistaParams(*[t.data_ptr() for t in params])
-        pg = _lib.CistaParamGrads(*[t.data_ptr() for t in pgrads])
+        pg = _lib.CistaParamGrads(*[g_flat.data_ptr() + 4 * o for o in offs])
         ws = model.train_workspace(B, H, W, dev)
         _lib.check(L.cista_backward(ctypes_ref(cfg), model.packed_params().data_ptr(), ctypes_ref(cp_),
                                     B, H, W, ctypes_ref(io), saved.data_ptr(), saved.numel(),
@@ -287,7 +325,7 @@ class _CistaFrame(torch.autograd.Function):
                                     _lib.stream_handle(dev)), "cista_backward")
         # keep the host-side argument tensors alive until the stream has consumed them
         model._bwd_keepalive = (params, g_rec, g_cl, g_z, g_h, g_c)
-        return (None, g_ev, g_pi, g_clp, g_zp, g_hp, g_cp, *pgrads)
+        return (None, g_ev, g_pi, g_clp, g_zp, g_hp, g_cp, g_flat if need[7] else None)
 
 
 def _train_frame(model, events, prev_image, prev_states):
@@ -312,5 +350,5 @@ def _train_frame(model, events, prev_image, prev_states):
             _check_input(f"prev_states[{i}]", t, shp, dev)
     if (sts[2] is None) != (sts[3] is None):
         raise RuntimeError("prev_states[2] must be None or an (h, c) pair")
-    rec, c_lstc, z, hs, cs = _CistaFrame.apply(model, events, prev_image, *sts, *model._unique_params())
+    rec, c_lstc, z, hs, cs = _CistaFrame.apply(model, events, prev_image, *sts, model._grad_conduit())
     return rec, [c_lstc, z, (hs, cs)]
