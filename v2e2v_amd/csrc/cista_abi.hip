@@ -417,7 +417,7 @@ struct Frame {
     float *rec, *pre;
     // training forward: activations saved for the backward (all NULL at inference)
     float *gi, *gf, *go;   // ConvLSTC gates (sigmoid)                    (B,h,w,2C) each
-    float *zl;             // ConvLSTC output = ISTA z_0                  (B,h,w,2C)
+    float *zl;             // depth x ISTA z_k, z_0 = ConvLSTC output      (B,h,w,2C)
     float *v;              // depth x pre-softshrink ISTA values          (B,h,w,2C)
     float *xs;             // depth x ISTA x_k = x1 - D(z_k)              (B,h,w,C)
     float *y;              // relu(Dg.conv(z))                            (B,h,w,C)
@@ -467,7 +467,11 @@ ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int
 
 int run_layer(const Frame &f, int layer, int it = 0) {
     const size_t hw = (size_t)f.B * f.h * f.w;
-    const bool zl_in = f.zl && it == 0 && f.cfg->depth > 0;   // ISTA iteration 0 reads z_0
+    // training: the ISTA iterates z_0 .. z_{D-1} stay in the saved stack at f.zl (the backward's
+    // D wgrad inputs), iteration `it` reading slot it and writing slot it+1 (the last one f.z)
+    const bool zstack = f.zl && f.cfg->depth > 0;
+    float *z_in = zstack ? f.zl + (size_t)it * hw * 2 * f.C : f.z;
+    float *z_out = zstack && it + 1 < f.cfg->depth ? f.zl + (size_t)(it + 1) * hw * 2 * f.C : f.z;
     const int C = f.C, B = f.B, h = f.h, w = f.w;
     ConvArgs a;
     switch (layer) {
@@ -583,13 +587,13 @@ int run_layer(const Frame &f, int layer, int it = 0) {
             a.out0 = (f.zl && f.cfg->depth > 0) ? f.zl : f.z; a.aux0 = f.c_lstc; a.out1 = f.go;
             return launch_conv<STAGE_S1, EPI_LSTC_OUT, 1>(a, f.st);
         case CISTA_LAYER_ISTA_D:    // x = x1 - D(z)                              e2v_model.py:73-74
-            a = conv_args_f(f, CV_D, C, B, h, w, h, w, zl_in ? f.zl : f.z, 2 * C, nullptr, 0);
+            a = conv_args_f(f, CV_D, C, B, h, w, h, w, z_in, 2 * C, nullptr, 0);
             a.out0 = f.xs ? f.xs + it * hw * C : f.xb; a.aux0 = f.x1;
             return launch_conv<STAGE_S1, EPI_ISTA_D, 1>(a, f.st);
         case CISTA_LAYER_ISTA_P:    // z = softshrink(P(x) + z, lambda)            :75-77
             a = conv_args_f(f, CV_P, C, B, h, w, h, w, f.xs ? f.xs + it * hw * C : f.xb, C,
                           nullptr, 0);
-            a.out0 = f.z; a.aux0 = zl_in ? f.zl : f.z; a.lambda = blob<float>(f.packed, f.L.lambda);
+            a.out0 = z_out; a.aux0 = z_in; a.lambda = blob<float>(f.packed, f.L.lambda);
             a.out1 = f.v ? f.v + it * hw * 2 * C : nullptr;
             return launch_conv<STAGE_S1, EPI_ISTA_P, 1>(a, f.st);
         case CISTA_LAYER_DG:        // y = relu(Dg.conv(z))                      base_layers.py:222
@@ -747,7 +751,7 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.gi = take(hw * 2 * C);
     s.gf = take(hw * 2 * C);
     s.go = take(hw * 2 * C);
-    s.zl = take(hw * 2 * C);
+    s.zl = take(hw * 2 * C * (D > 0 ? D : 1));   // z_0 = ConvLSTC output, then the ISTA iterates
     s.v = take(hw * 2 * C * (D > 0 ? D : 1));
     s.xs = take(hw * C * (D > 0 ? D : 1));
     s.y = take(hw * C);
@@ -764,7 +768,7 @@ constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per lau
 constexpr int SCL_PAIRS = 16;                // scale pairs of the non-ISTA gradients of a call (8 used)
 
 struct BwdWs {
-    float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *zk, *gx1, *Go, *gz0;
+    float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *gx1, *Go, *gz0;
     float *part, *bpart, *dlp;
     float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
     unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses)
@@ -796,7 +800,6 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     const size_t nd = cfg.depth > 0 ? (size_t)cfg.depth : 1;
     s.gv = take(nd * hw * 2 * C);
     s.gxk = take(nd * hw * C);
-    s.zk = take(nd * hw * 2 * C);
     s.gx1 = take(hw * C);
     s.Go = take(hw * 2 * C);
     s.gz0 = take(hw * 2 * C);
@@ -1181,12 +1184,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     for (int it = D - 1; it >= 0; --it) {
         const float *v = sv.v + (size_t)it * hw * 2 * C;
         float *gv = ws.gv + (size_t)it * hw * 2 * C, *gxk = ws.gxk + (size_t)it * hw * C;
-        float *zk = ws.zk + (size_t)it * hw * 2 * C;      // D's input of this iteration (its wgrad X)
-        if (it > 0)
-            hipLaunchKernelGGL(softshrink_fwd4_kernel, g1d(hw * 2 * C / 4), dim3(256), 0, st,
-                               sv.v + (size_t)(it - 1) * hw * 2 * C, lam, zk, hw, 2 * C);
-        else if (hipMemcpyAsync(zk, sv.zl, (size_t)hw * 2 * C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
-            return CISTA_ERR_HIP;
         if (1024 % (2 * C) == 0)
             hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
                                lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
@@ -1215,7 +1212,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0, pg.P_b, sP,
                            D * B));
-        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, ws.zk, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
+        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, sv.zl, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
                            D * B));
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------

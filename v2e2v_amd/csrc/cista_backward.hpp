@@ -1611,17 +1611,6 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
     if (amax) amax_publish(amax, mx);
 }
 
-// z = softshrink(v, lambda) over float4 channel groups (C % 4 == 0)
-__global__ void softshrink_fwd4_kernel(const float *v, const float *lam, float *z, long npix, int C) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const int cq = C >> 2;
-    if (i >= npix * cq) return;
-    const int c = (int)(i % cq) * 4;
-    const float4 x = reinterpret_cast<const float4 *>(v)[i];
-    reinterpret_cast<float4 *>(z)[i] = make_float4(softshrink_(x.x, lam[c]), softshrink_(x.y, lam[c + 1]),
-                                                   softshrink_(x.z, lam[c + 2]), softshrink_(x.w, lam[c + 3]));
-}
-
 // dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel;
 // one workgroup per channel, tree reduction
 __global__ __launch_bounds__(256) void lambda_grad_kernel(const float *dlp, int nbl, int C, float *dst,
