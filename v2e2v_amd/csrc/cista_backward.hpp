@@ -1628,14 +1628,6 @@ __global__ __launch_bounds__(256) void lambda_grad_kernel(const float *dlp, int 
     if (threadIdx.x == 0) dst[c] = (accumulate ? dst[c] : 0.0f) + red[0];
 }
 
-// z = softshrink(v, lambda) (recompute of the ISTA iterate for the D wgrad)
-__global__ void softshrink_fwd_kernel(const float *v, const float *lam, float *z, long npix, int C) {
-    const long i = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= npix * C) return;
-    const float x = v[i], l = lam[i % C];
-    z[i] = softshrink_(x, l);
-}
-
 // ConvLSTC cell backward (reference base_layers.py:52-71), per (pixel, channel), Cz = 2C:
 // saved i, f (post-sigmoid, Cz each), o (Cz), z0, c (cell), c_prev (nullable);
 // gz: grad of the LSTC output z (= ISTA z_0); gcl: grad of c (from the next frame, nullable).
