@@ -396,8 +396,11 @@ struct RawScratch {
     unsigned long long *totb;      // [B][MAXSLOTS][SLOTW/2] partial event totals per element
     unsigned long long *run;       // [B] next output row of each element, [B] the call's total
     int *mis;                      // [CISTA_V2E_MAX_FRAMES] max_num_iters of each frame step
+    unsigned *tsum;                // [B][ntiles] tile sums of cnt, then the tiles' first rows
     int nchunks;                   // 64-pixel waves per batch element
+    int ntiles;                    // SCAN_TILE-element tiles of one element's cnt
 };
+constexpr int SCAN_TILE = 4096;    // 256 threads x 16 consecutive counts
 
 // One wave = 64 consecutive pixels of one element (grid (ceil(nchunks / 4), B)).  COUNT: the
 // frame step with its state update, adding the events to the element's total.  Otherwise the
@@ -466,20 +469,51 @@ __global__ void v2e_raw_offsets_kernel(RawScratch r, int B) {
     r.run[B] = acc;
 }
 
-// One workgroup per element: the counts [32][nchunks] (iteration-major, then pixel order) become
-// exclusive row offsets starting at run[b], which then moves past this block's rows.
-__global__ __launch_bounds__(1024) void v2e_raw_scan_kernel(RawScratch r) {
+// The counts [32][nchunks] of an element (iteration-major, then pixel order) become exclusive
+// row offsets continuing from run[b], in three launches over SCAN_TILE-count tiles: tile sums,
+// one workgroup per element scanning its tile sums (and moving run[b] past this block's rows),
+// then each tile rescanned from its offset.
+__device__ __forceinline__ unsigned block_excl_scan256(unsigned v, unsigned *wsum, unsigned &total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    unsigned incl = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const unsigned t = __shfl_up(incl, o);
+        if (lane >= o) incl += t;
+    }
+    if (lane == 63) wsum[wv] = incl;
+    __syncthreads();
+    unsigned before = 0;
+    for (int k = 0; k < wv; ++k) before += wsum[k];
+    total = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+    return before + incl - v;
+}
+
+__global__ __launch_bounds__(256) void v2e_raw_tile_sum_kernel(RawScratch r) {
+    __shared__ unsigned wsum[4];
+    const int b = blockIdx.y, n = 32 * r.nchunks;
+    const unsigned *a = r.cnt + (size_t)b * n;
+    const int base = blockIdx.x * SCAN_TILE + threadIdx.x * 16;
+    unsigned v = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k)
+        if (base + k < n) v += a[base + k];
+    unsigned total;
+    block_excl_scan256(v, wsum, total);
+    if (threadIdx.x == 0) r.tsum[(size_t)b * r.ntiles + blockIdx.x] = total;
+}
+
+__global__ __launch_bounds__(1024) void v2e_raw_tile_scan_kernel(RawScratch r) {
     __shared__ unsigned wsum[16];
     const int b = blockIdx.x;
-    const int n = 32 * r.nchunks;
-    unsigned *a = r.cnt + (size_t)b * n;
+    const int n = r.ntiles;
+    unsigned *a = r.tsum + (size_t)b * n;
     const int per = (n + 1023) / 1024;
     const int lo = min(n, (int)threadIdx.x * per), hi = min(n, lo + per);
     const unsigned long long start = r.run[b];       // read before the barrier, written after
     unsigned sum = 0;
     for (int k = lo; k < hi; ++k) sum += a[k];
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-    unsigned v = sum;                                 // inclusive scan within the wave
+    unsigned v = sum;
     for (int o = 1; o < 64; o <<= 1) {
         const unsigned t = __shfl_up(v, o);
         if (lane >= o) v += t;
@@ -495,6 +529,26 @@ __global__ __launch_bounds__(1024) void v2e_raw_scan_kernel(RawScratch r) {
         pos += x;
     }
     if (threadIdx.x == 1023) r.run[b] = start + before + v;
+}
+
+__global__ __launch_bounds__(256) void v2e_raw_tile_apply_kernel(RawScratch r) {
+    __shared__ unsigned wsum[4];
+    const int b = blockIdx.y, n = 32 * r.nchunks;
+    unsigned *a = r.cnt + (size_t)b * n;
+    const int base = blockIdx.x * SCAN_TILE + threadIdx.x * 16;
+    unsigned c[16], v = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        c[k] = base + k < n ? a[base + k] : 0u;
+        v += c[k];
+    }
+    unsigned total;
+    unsigned pos = r.tsum[(size_t)b * r.ntiles + blockIdx.x] + block_excl_scan256(v, wsum, total);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        if (base + k < n) a[base + k] = pos;
+        pos += c[k];
+    }
 }
 
 // The rows of iteration block `blk`: an event's row is its (iteration, wave) offset plus its rank
@@ -610,6 +664,8 @@ RawScratch carve_raw(void *base, int B, int H, int W, size_t *bytes) {
     r.totb = static_cast<unsigned long long *>(take((size_t)B * MAXSLOTS * (SLOTW / 2) * 8));
     r.run = static_cast<unsigned long long *>(take(((size_t)B + 1) * 8));
     r.mis = static_cast<int *>(take(CISTA_V2E_MAX_FRAMES * 4));
+    r.ntiles = (32 * r.nchunks + SCAN_TILE - 1) / SCAN_TILE;
+    r.tsum = static_cast<unsigned *>(take((size_t)B * r.ntiles * 4));
     *bytes = off;
     return r;
 }
@@ -810,7 +866,10 @@ int cista_v2e_forward_raw(const cista_v2e_config *cfg, cista_v2e_host_state *hs,
             hipLaunchKernelGGL(v2e_raw_emit_kernel<false>, wgrid, dim3(256), 0, st, c, s, L.sc, r, frames, n, dt, blk,
                                blk == nblk - 1 ? 1 : 0);
             if (mis[n] == 0) continue;
-            hipLaunchKernelGGL(v2e_raw_scan_kernel, dim3((unsigned)B), dim3(1024), 0, st, r);
+            const dim3 tgrid((unsigned)r.ntiles, (unsigned)B);
+            hipLaunchKernelGGL(v2e_raw_tile_sum_kernel, tgrid, dim3(256), 0, st, r);
+            hipLaunchKernelGGL(v2e_raw_tile_scan_kernel, dim3((unsigned)B), dim3(1024), 0, st, r);
+            hipLaunchKernelGGL(v2e_raw_tile_apply_kernel, tgrid, dim3(256), 0, st, r);
             hipLaunchKernelGGL(v2e_raw_fill_kernel, wgrid, dim3(256), 0, st, c, L.sc, r, n, blk, events, capacity);
         }
         hs->t_previous = c.tf[n];
