@@ -95,6 +95,50 @@ def test_three_frame_bptt_l1(golden):
     assert not bad, bad
 
 
+def test_gradient_accumulation_across_sequences(golden):
+    """The frames reach the parameters through one flat conduit tensor per parameter version
+    (CistaLSTCNet._grad_conduit), dropped once its gradient is computed.  Two sequences
+    backpropagated one after the other without an optimizer step accumulate gA + gB; both
+    forwarded first and backpropagated through one summed loss give the same; a forward with
+    grad enabled and no backward changes nothing."""
+    d = golden("grads_32x48.npz")
+    m = model()
+    B, _, H, W = d["g2_target"].shape
+    tgt = gpu(d["g2_target"])
+
+    def seq(order):
+        prev = torch.zeros(B, 1, H, W, device=DEV)
+        state = None
+        for s in order:
+            out, state = m(gpu(d["voxels"][s]), prev, state)
+            prev = out.clone()
+        return torch.nn.functional.l1_loss(out, tgt)
+
+    def grads():
+        torch.cuda.synchronize()
+        return {k: p.grad.detach().clone() for k, p in m.named_parameters()}
+
+    m.zero_grad(set_to_none=True)
+    seq([0, 1, 2]).backward()
+    ga = grads()
+    m.zero_grad(set_to_none=True)
+    seq([2, 1, 0]).backward()
+    gb = grads()
+    m.zero_grad(set_to_none=True)
+    seq([1, 0]).sum()                                  # forward with grad, never backpropagated
+    seq([0, 1, 2]).backward()
+    seq([2, 1, 0]).backward()
+    acc = grads()
+    m.zero_grad(set_to_none=True)
+    (seq([0, 1, 2]) + seq([2, 1, 0])).backward()
+    joint = grads()
+    for k in ga:
+        want = (ga[k] + gb[k]).cpu().numpy()
+        assert rel_err(acc[k].cpu().numpy(), want) < 1e-6, k
+        assert rel_err(joint[k].cpu().numpy(), want) < 1e-5, k
+        assert acc[k].shape == dict(m.named_parameters())[k].shape
+
+
 def test_training_forward_equals_inference_forward(golden):
     d = golden("grads_32x48.npz")
     m = model()
