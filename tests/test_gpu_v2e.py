@@ -225,11 +225,17 @@ def test_raw_random_configuration_matches_voxel_mode():
     fr = torch.from_numpy(video(2, 10, 64, 80, seed=3)).cuda()
     tf = torch.from_numpy(times(2, 10, 0.0))
     raw = [v2e.EventEmulator("raw", device="cuda", seed=11, **cfg)(fr, tf) for _ in range(2)]
-    _, n_vox = v2e.EventEmulator("voxel_grid", device="cuda", seed=11, **cfg)(fr, tf)
+    vox, n_vox = v2e.EventEmulator("voxel_grid", device="cuda", seed=11, **cfg)(fr, tf)
     assert raw[0][1] == raw[1][1] == n_vox > 0 and torch.equal(raw[0][0], raw[1][0])
     ev = raw[0][0].cpu().numpy()
     key = np.lexsort((ev[:, 1], ev[:, 2], ev[:, 0], ev[:, 4]))
     assert np.array_equal(key, np.arange(len(ev)))
+    # the same events: the rows scattered with the reference's voxel arithmetic and normalised
+    # give the voxel mode's grid (noise, leak and refractory draws included)
+    from tests.test_oracle_v2e_raw import scatter
+    ref = vo.preprocess_whole(scatter(ev, 2, 5, 64, 80))
+    got = vox.cpu().numpy()
+    assert np.abs(got - ref).max() <= TOL * max(1.0, np.abs(ref).max())
 
 
 def test_raw_static_video_returns_1d_empty():
