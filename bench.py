@@ -230,7 +230,7 @@ def v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt, min_s=10.0, max_re
     from oracle import fixtures as fx
     from oracle import v2e_oracle as vo
     from oracle.cista_oracle_torch import CistaLSTCTorchCPU
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    cores, core_note = host_cores()
     torch.set_num_threads(cores)
     e2v = net.e2v_net
     sd = {k: v.detach().cpu().numpy() for k, v in e2v.state_dict().items()}
@@ -252,7 +252,7 @@ def v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt, min_s=10.0, max_re
     return dict(value=recs / t, unit="frames/s", cores=int(cores), kind="port",
                 sample=f"{recs} reconstruction(s) at {H}x{W} (B=1), each a {P}-frame pack through the numpy "
                        f"emulator restatement (oracle/v2e_oracle.py) + the PyTorch-CPU CISTA-LSTC restatement "
-                       f"(oracle/cista_oracle_torch.py), {cores} threads, {t:.1f} s")
+                       f"(oracle/cista_oracle_torch.py), {core_note}, {t:.1f} s")
 
 
 def train_main(args, torch, vd, rank, world, device):
@@ -401,7 +401,7 @@ def train_cpu_baseline(torch, model, vox, target, L, H, W, min_s=10.0, max_steps
     same L frames and size -- on this host's cores, repeated to ~10 s."""
     from oracle import fixtures as fx
     from oracle.cista_oracle_torch import CistaLSTCTorchCPU, bptt_step
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    cores, core_note = host_cores()
     torch.set_num_threads(cores)
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
     net = CistaLSTCTorchCPU(fx.collapse_tied(sd, model.depth), model.depth, requires_grad=True)
@@ -415,7 +415,7 @@ def train_cpu_baseline(torch, model, vox, target, L, H, W, min_s=10.0, max_steps
         steps += 1
     return dict(value=steps * L / dt, unit="frames/s", cores=int(cores), kind="port",
                 sample=f"{steps} BPTT step(s) of {L} frames at {H}x{W}, B=1 (L1 on the last frame, "
-                       f"autograd through the PyTorch-CPU restatement), {cores} threads, {dt:.1f} s")
+                       f"autograd through the PyTorch-CPU restatement), {core_note}, {dt:.1f} s")
 
 
 # ------------------------------------------------------------------ synthetic inputs (GPU)
@@ -604,6 +604,28 @@ def dominant_roofline(layers, lib_mod, traffic_tag=None):
     return roofline
 
 
+def host_cores():
+    """Threads for a cpu_baseline leg (every core the process may run on): all of
+    os.sched_getaffinity, capped by the cgroup's CPU quota (cpu.max) when there is one -- the
+    cores actually granted -- and by OMP_NUM_THREADS only when that is set explicitly.  Returns
+    (threads, note naming the three numbers)."""
+    aff = len(os.sched_getaffinity(0))
+    quota = None
+    try:
+        q, per = open("/sys/fs/cgroup/cpu.max").read().split()[:2]
+        if q != "max":
+            quota = max(1, math.ceil(int(q) / int(per)))
+    except (OSError, ValueError):
+        pass
+    omp = os.environ.get("OMP_NUM_THREADS")
+    n = aff if quota is None else min(aff, quota)
+    if omp and omp.isdigit() and int(omp) > 0:
+        n = min(n, int(omp))
+    note = (f"{n} threads of {aff} affine cores (cgroup quota {quota if quota else 'none'}, "
+            f"OMP_NUM_THREADS {omp if omp else 'unset'})")
+    return n, note
+
+
 def psnr(a, b):
     """utils/evaluate.py:18-28 (PIXEL_MAX = 1, 100 if mse < 1e-10)."""
     import numpy as np
@@ -620,7 +642,7 @@ def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
     import numpy as np
     from oracle import fixtures as fx
     from oracle.cista_oracle_torch import CistaLSTCTorchCPU
-    cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+    cores, core_note = host_cores()
     torch.set_num_threads(cores)
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
     ref = CistaLSTCTorchCPU(fx.collapse_tied(sd, model.depth), model.depth)
@@ -646,11 +668,13 @@ def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
             g_recs.append(prev.cpu().numpy())
     g_recs = np.stack(g_recs)
     rel = float(np.abs(g_recs - o_recs).max() / np.abs(o_recs).max())
+    # SURVEY 7's frame metric: per pixel, each against its own magnitude
+    erel = float((np.abs(g_recs.astype(np.float64) - o_recs) / np.maximum(np.abs(o_recs), 1e-30)).max())
     ps = float(np.mean([psnr(g_recs[f], o_recs[f]) for f in range(n_frames)]))
     return dict(value=frames / dt, unit="frames/s", cores=int(cores), kind="port",
                 sample=f"{seqs} sequence(s) x {n_frames} recurrent frames at {H}x{W} (B=1), "
                        f"PyTorch-CPU op-for-op restatement (oracle/cista_oracle_torch.py), "
-                       f"{cores} threads, {dt:.1f} s"), ps, rel
+                       f"{core_note}, {dt:.1f} s"), ps, rel, erel
 
 
 def frame_work(lib_mod, model, H, W):
@@ -759,9 +783,9 @@ def main():
                  if rank == 0 else None)
 
     cpu = None
-    psnr_vs_ref = rel_vs_ref = None
+    psnr_vs_ref = rel_vs_ref = erel_vs_ref = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu, psnr_vs_ref, rel_vs_ref = cpu_baseline(torch, model, vox, H, W,
+        cpu, psnr_vs_ref, rel_vs_ref, erel_vs_ref = cpu_baseline(torch, model, vox, H, W,
                                                     min(args.cpu_frames, L))
 
     if rank == 0:
@@ -806,6 +830,7 @@ def main():
                 "hbm_gbps_algorithmic": round(value / world * bytes_frame / 1e9, 1)},
             "psnr_vs_ref": None if psnr_vs_ref is None else round(psnr_vs_ref, 2),
             "max_rel_err_vs_ref": rel_vs_ref,
+            "max_elementwise_rel_err_vs_ref": erel_vs_ref,
             "outputs_finite": finite,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -51,11 +51,13 @@ enum {
  * H x W frame (its np.add.at on the flat index x + y W + bin H W, utils/event_process.py:53-58) */
 enum {
     CISTA_VOXEL_OUT_OF_RANGE = 1,  /* a flat index (np.uint: truncated, wrapped modulo 2^64, read
-                                      back as intp) outside [-size, size): the reference raises
-                                      IndexError                                                */
-    CISTA_VOXEL_SPILL = 2          /* a flat index inside [-size, size): the reference adds the
-                                      event to another pixel / bin (a negative index counts from
-                                      the end of the grid); this build drops it                  */
+                                      back as intp) outside [-size, size) -- for the torch twin
+                                      outside [0, size): the reference raises IndexError; the
+                                      event is dropped here                                     */
+    CISTA_VOXEL_SPILL = 2          /* a flat index inside the grid: the reference adds the event
+                                      to another pixel / bin (a negative numpy index counts from
+                                      the end of the grid), and so does this build, in event
+                                      order with that cell's own events (bit-identical)         */
 };
 
 /* Workspace for cista_voxelize: n_events = total events of the batch (offsets[B]). */
@@ -71,9 +73,9 @@ size_t cista_voxel_workspace_bytes(int B, long long n_events, int num_bins, int 
  * mode     : CISTA_VOXEL_*; hot_threshold > 0 zeroes |v| > hot_threshold before normalising
  *            (reference: 25/num_bins for event_preprocess(filter_hot_pixel=True),
  *            20/num_bins for event_preprocess_pytorch); <= 0 disables the filter.
- * Events whose x, y fall outside the H x W frame are dropped; cista_voxelize_checked reports
- * them (grid_status).  The input is never modified (the reference rewrites events[:, 0] and the
- * polarity column).
+ * Events whose x, y fall outside the H x W frame are added where the reference's flat index puts
+ * them, or dropped where the reference raises; cista_voxelize_checked reports which (grid_status).
+ * The input is never modified (the reference rewrites events[:, 0] and the polarity column).
  */
 int cista_voxelize(const double *events, const long long *offsets, int B, long long n_events, int num_bins,
                    int height, int width, int mode, float hot_threshold, float *voxels, void *workspace,

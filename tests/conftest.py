@@ -32,3 +32,12 @@ def rel_err(a, ref):
     a = np.asarray(a, np.float64)
     ref = np.asarray(ref, np.float64)
     return float(np.abs(a - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def elem_rel_err(a, ref):
+    """max over elements of |a - ref| / |ref|: the frame metric of SURVEY section 7 (frames lie in
+    (0, 1), so each pixel is held to its own magnitude -- a dark pixel of 1e-3 may not be off by
+    1e-7 absolute more than 1e-4 of itself).  Not for states, which contain exact zeros."""
+    a = np.asarray(a, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float((np.abs(a - ref) / np.maximum(np.abs(ref), 1e-30)).max())

@@ -91,6 +91,8 @@ def _loader_worker(rank, world, port, q):
     ld = data.GpuVoxelLoader(ds, "cpu", batch_size=1)
     res["world"] = (ld.rank, ld.world_size, len(ld))
     res["plain"] = [_seq_of(ds, it[0][0]) for it in ld.loader]
+    # world_size given without rank: the rank still comes from the process group (not 0 everywhere)
+    res["ws_only_rank"] = data.GpuVoxelLoader(ds, "cpu", batch_size=1, world_size=world).rank
     ld = data.GpuVoxelLoader(ds, "cpu", batch_size=1, shuffle=True, seed=5)
     for ep in (0, 1):
         ld.set_epoch(ep)
@@ -132,6 +134,18 @@ def test_gloo_loader_shards_are_disjoint_and_cover_the_split():
     assert g[0]["plain"] == [0, 2, 4] and g[1]["plain"] == [1, 3, 5]
     assert g[0]["shuf0"] != g[0]["shuf1"] or g[1]["shuf0"] != g[1]["shuf1"]   # reshuffled per epoch
     assert g[0]["ragged"] == "refused"                           # sequences 0 (6 frames) + 2 (5 frames)
+    assert [r["ws_only_rank"] for r in g] == [0, 1]
+
+
+def test_loader_needs_a_rank_for_world_size():
+    """world_size > 1 with no rank and no process group would put every process on shard 0."""
+    from v2e2v_amd import data
+    ds = _tiny_dataset()
+    with pytest.raises(ValueError):
+        data.GpuVoxelLoader(ds, "cpu", batch_size=1, world_size=2)
+    with pytest.raises(ValueError):
+        data.GpuVoxelLoader(ds, "cpu", batch_size=1, world_size=2, rank=2)
+    assert data.GpuVoxelLoader(ds, "cpu", batch_size=1, world_size=2, rank=1).rank == 1
 
 
 def test_sequence_shard_sampler_properties():

@@ -6,8 +6,11 @@ std-normalised voxels of the other parity tests:
   reference restatement (oracle/cista_oracle_torch.py, pinned to the golden vectors);
 * conv inputs far beyond the fp16 range of the split's hi part (|x| >= 65520): every stage of
   the frame, fed such inputs through the C ABI, matches the fp64 oracle within 1e-4 (the range
-  pass recomputes those tiles on the exact fp32 MFMA; tiles of the other sample in the same
-  launch stay on the split path);
+  pass recomputes those tiles on the same split-f16 MFMAs with power-of-two pre-scaled inputs,
+  one scale per magnitude class; tiles of the other sample in the same launch stay on the split
+  path);
+* one outlier (1e6, 1e12) inside a tile of O(1) values: the O(1) outputs of that tile keep their
+  own accuracy (the range pass's magnitude classes);
 * weights x3 / x100 and voxels x1e4 drive the reference's own activations to 3e6 .. 1e23: the
   module returns every frame (nothing raised, nothing refused) and each output is as close to
   the fp64 truth as the reference's fp32 CPU paths are (they themselves drift by up to 1.0
@@ -24,7 +27,7 @@ import torch
 from oracle import fixtures as fx
 from oracle.cista_oracle_torch import CistaLSTCTorchCPU
 from oracle.cista_oracle import CistaLSTCOracle, relu, reflect_pad1, upsample_bilinear2x
-from tests.conftest import rel_err
+from tests.conftest import elem_rel_err, rel_err
 from v2e2v_amd import CistaLSTCNet, _lib
 
 pytestmark = pytest.mark.gpu
@@ -122,7 +125,7 @@ def _nchw(t):
 @pytest.mark.parametrize("stage", ["input", "lstc", "lstc_none", "ista", "decoder", "decoder_none", "output"])
 def test_range_pass_stages_match_fp64(stage):
     """Every conv of the frame with inputs ~1e6 in sample 0 (beyond the fp16 hi part: those
-    tiles take the fp32-MFMA re-run) and normal inputs in sample 1, at a size whose tiles are
+    tiles take the pre-scaled range pass) and normal inputs in sample 1, at a size whose tiles are
     ragged (40 x 56), against the fp64 oracle.  Bar per tensor and sample: 1e-4, or 3x the error
     of the fp32 restatement of the same stage where the saturating gates make the stage itself
     ill-conditioned (pre-activations of ~1e7 cancelling to O(1))."""
@@ -205,6 +208,66 @@ def test_range_pass_stages_match_fp64(stage):
                 assert rel_err(g[b], r[b]) < TOL, (stage, k, b, rel_err(g[b], r[b]))
             else:
                 as_close_as_fp32(g[b], r[b], [r32[b]], (stage, k, b))
+
+
+@pytest.mark.parametrize("outlier", [1e6, 1e12])
+@pytest.mark.parametrize("stage", ["ista", "decoder"])
+def test_range_pass_outlier_inside_tile(stage, outlier):
+    """ONE huge value (z0[channel 5] at pixel (10, 14)) among O(1) conv inputs, so the tile that
+    holds it mixes magnitudes: that tile takes the range pass, and its outputs that do not see the
+    outlier (Chebyshev distance > 5 from it: 2 ISTA iterations = 4 convs, or Dg + the gate conv)
+    must keep their own accuracy.  With one power-of-two scale per tile, an O(1) value beside 1e12
+    would be scaled to 1.5e-8 -- below the smallest fp16 subnormal -- and vanish.  Bars against the
+    fp64 oracle, on those far outputs: max-normalised 1e-4 over the far region (not over the
+    tensor, whose max is the outlier's neighbourhood), and elementwise 1e-4 on every far output of
+    at least 1 % of that max (the reference's own fp32 path: 6e-7 and 4e-5); the near outputs hold
+    1e-4 of their own region's max."""
+    B, h, w, C = 1, 20, 28, 64
+    params = fx.stress_params(C, 5, 5, seed=7)
+    m = make_model(params)
+    packed = m.packed_params()
+    ws = m.workspace(B, 2 * h, 2 * w, torch.device(DEV))
+    cfg = _lib.CistaConfig(C, 5, 5)
+    L = _lib.lib()
+    rng = np.random.default_rng(4)
+    x1 = rng.standard_normal((B, C, h, w)).astype(np.float32)
+    z0 = rng.standard_normal((B, 2 * C, h, w)).astype(np.float32)
+    z0[rng.random(z0.shape) < 0.3] = 0.0
+    z0[0, 5, 10, 14] = outlier
+
+    def call(fn, *args):
+        _lib.check(fn(ctypes.byref(cfg), packed.data_ptr(), *args, ws.data_ptr(), ws.numel(), None), fn.__name__)
+        torch.cuda.synchronize()
+
+    if stage == "ista":
+        tx, tz = _nhwc(x1), _nhwc(z0)
+        call(L.cista_stage_ista, B, h, w, tx.data_ptr(), tz.data_ptr(), 2)
+        got = [_nchw(tz)]
+
+        def ref_fn(o):
+            zz, xd = z0.astype(o.dtype), x1.astype(o.dtype)
+            for _ in range(2):
+                x = o._conv("lista.P.conv2d", xd - o._conv("lista.D.conv2d", zz)) + zz
+                zz = np.maximum(x - o.p["lista.Lambda"], 0) - np.maximum(-x - o.p["lista.Lambda"], 0)
+            return [zz]
+    else:
+        hs, cs = torch.empty(B, h, w, C, device=DEV), torch.empty(B, h, w, C, device=DEV)
+        tz = _nhwc(z0)
+        call(L.cista_stage_decoder, B, h, w, tz.data_ptr(), None, None, hs.data_ptr(), cs.data_ptr())
+        got = [_nchw(hs), _nchw(cs)]
+        ref_fn = lambda o: list(o.lstm(relu(o._conv("Dg.conv.conv2d", z0.astype(o.dtype))), None))  # noqa: E731
+    with np.errstate(over="ignore"):
+        truth = ref_fn(CistaLSTCOracle(params, 5, dtype=np.float64))
+    yy, xx = np.mgrid[0:h, 0:w]
+    far = np.maximum(np.abs(yy - 10), np.abs(xx - 14)) > 5
+    for k, (g, t) in enumerate(zip(got, truth)):
+        assert np.isfinite(g).all(), k
+        gf, tf = g[0][:, far], t[0][:, far]
+        mf = np.abs(tf).max()
+        assert np.abs(gf - tf).max() / mf < TOL, (k, np.abs(gf - tf).max() / mf)
+        sig = np.abs(tf) >= 1e-2 * mf
+        assert elem_rel_err(gf[sig], tf[sig]) < TOL, (k, elem_rel_err(gf[sig], tf[sig]))
+        assert rel_err(g[0][:, ~far], t[0][:, ~far]) < TOL, k
 
 
 @pytest.mark.parametrize("wscale,vscale", [(3.0, 1.0), (100.0, 1.0), (1.0, 1e4)])

@@ -72,19 +72,17 @@ def test_edge_cases():
     H, W, nb = 20, 30, 5
     # all events at one timestamp (deltaT == 0 -> 1.0, reference :40-41), polarity given as -1/1
     ev0 = np.array([[0.5, 3, 4, 1], [0.5, 3, 4, -1], [0.5, 29, 19, 0], [0.5, 0, 0, 1]], np.float64)
-    # fractional coordinates truncate toward zero (astype(np.uint)); out-of-grid events dropped
+    # fractional coordinates truncate toward zero (astype(np.uint)); x = W and y = H are inside
+    # the flat grid: the reference adds them to other pixels / bins, and so does this build
     ev1 = np.array([[0.0, 2.7, 1.2, 1], [0.01, 29.99, 19.5, 0], [0.02, 30.0, 2, 1], [0.03, 1, 20, 1],
                     [0.04, -0.5, 3, 1], [0.05, 5, 5, 1]], np.float64)
-    ev1_kept = ev1[[0, 1, 4, 5]].copy()
-    ev1_kept[2, 1] = 0.0                         # -0.5 truncates to 0, like the reference's cast
-    # x = W and y = H are inside the flat grid: the reference adds them to other pixels / bins,
-    # this build drops them and says so
-    with pytest.warns(RuntimeWarning, match="dropped"):
-        got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H).cpu().numpy()
+    got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H).cpu().numpy()
     assert_bits(got[0], ref_raw(ev0, nb, W, H))
-    assert_bits(got[1], ref_raw(ev1_kept, nb, W, H))
+    assert_bits(got[1], ref_raw(ev1, nb, W, H))
     got = ep.events_to_voxel_batch([ev0, ev1], nb, W, H, strict=False).cpu().numpy()   # no check
-    assert_bits(got[1], ref_raw(ev1_kept, nb, W, H))
+    assert_bits(got[1], ref_raw(ev1, nb, W, H))
+    ev1_in = ev1[[0, 1, 4, 5]]
+    assert not np.array_equal(ref_raw(ev1, nb, W, H), ref_raw(ev1_in, nb, W, H))      # they do land
 
 
 @pytest.mark.parametrize("bad", ["negative_x", "beyond_grid", "last_bin_row_below"])
@@ -107,11 +105,38 @@ def test_out_of_grid_raises_like_reference(bad):
             ep.events_to_voxel_batch([ev], nb, W, H)
         ep.events_to_voxel_batch([ev], nb, W, H, strict=False)     # unchecked: the event is dropped
     # a negative x whose flat index stays inside [-size, size) lands elsewhere in the reference
-    # (moved back a row, or counted from the end of the grid): a spill
+    # (moved back a row, or counted from the end of the grid): a spill, reproduced bit for bit
     ev = np.array([[0.0, -3, 0, 1], [0.01, -3, 5, 0], [0.04, 1, 1, 1]], np.float64)
-    fx.voxelize(ev, nb, 30, 20)
-    with pytest.warns(RuntimeWarning, match="dropped"):
-        ep.events_to_voxel_batch([ev], nb, 30, 20)
+    assert_bits(ep.events_to_voxel_batch([ev], nb, 30, 20)[0].cpu().numpy(), fx.voxelize(ev, nb, 30, 20))
+
+
+@pytest.mark.parametrize("torch_semantics", [False, True])
+def test_spill_matches_reference(golden, torch_semantics):
+    """Events outside the frame whose flat index stays inside the grid (x >= W, y >= H, negative
+    x): the reference's np.add.at / index_add_ add them to the cell that index names, in event
+    order with the cell's own events.  Against grids the reference itself produced
+    (tests/golden/make_golden_spill.py): a 20 x 30 window (fused path), one whose negative index
+    wraps to the end of the grid (numpy; the torch twin raises there), a 64 x 64 window of three
+    sorted segments, and 520 x 520 (global-sort path) -- each alone and the small ones batched."""
+    d = golden("vox_spill.npz")
+    wins, shapes = [], []
+    for k in range(4):
+        nb, H, W = (int(v) for v in d[f"shape_{k}"])
+        ev = d[f"events_{k}"]
+        want = d[f"torch_{k}" if torch_semantics else f"np_{k}"]
+        if torch_semantics and not int(d[f"torch_ok_{k}"]):
+            with pytest.raises(IndexError):
+                ep.events_to_voxel_batch([ev], nb, W, H, torch_semantics=True)
+            continue
+        got = ep.events_to_voxel_batch([ev], nb, W, H, torch_semantics=torch_semantics)[0].cpu().numpy()
+        assert_bits(got, want)
+        if H == 20:
+            wins.append(ev)
+            shapes.append(want)
+    if len(wins) > 1:                     # per-window spill flags in one batched call
+        got = ep.events_to_voxel_batch(wins, 5, 30, 20, torch_semantics=torch_semantics).cpu().numpy()
+        for b, want in enumerate(shapes):
+            assert_bits(got[b], want)
 
 
 def test_preprocess_thresholds_and_batch_shapes():

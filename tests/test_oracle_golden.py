@@ -85,6 +85,20 @@ def test_voxelizer_matches_reference(golden):
     np.testing.assert_array_equal(fx.normalize_voxel(raw), d["voxel"])
 
 
+def test_voxelizer_spill_matches_reference(golden):
+    """Out-of-frame events that the reference's np.add.at adds to another pixel / bin (x >= W,
+    y >= H, negative x, a negative index wrapping to the grid's end): the restatement reproduces
+    the reference's own grids (tests/golden/make_golden_spill.py) bit for bit."""
+    d = golden("vox_spill.npz")
+    for k in range(4):
+        nb, H, W = (int(v) for v in d[f"shape_{k}"])
+        ev = d[f"events_{k}"]
+        outside = (ev[:, 1] <= -1) | (ev[:, 1] >= W) | (ev[:, 2] <= -1) | (ev[:, 2] >= H)
+        assert outside.sum() >= 90
+        got = fx.voxelize(ev, nb, W, H)
+        assert np.array_equal(got.view(np.uint32), d[f"np_{k}"].view(np.uint32)), k
+
+
 def test_primitives_vs_torch():
     rng = np.random.default_rng(0)
     x = rng.standard_normal((2, 6, 9, 11)).astype(np.float32)

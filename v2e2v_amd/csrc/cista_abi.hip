@@ -247,10 +247,10 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
         return CISTA_ERR_UNSUPPORTED;
     if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
     const size_t epi_lds = (size_t)NWV * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
-    // + 2 x NWV words of range-pass scratch right after the epilogue's LDS (inside the dead
-    // staging images when those are larger)
+    // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
+    // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    const size_t lds = t.lds > epi_lds + 8 * NWV ? t.lds : epi_lds + 8 * NWV;
+    const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
     hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
@@ -390,6 +390,12 @@ ConvArgs conv_args(const void *packed, const Layout &L, int id, int C, int B, in
     do {                                  \
         int _s = (x);                     \
         if (_s != CISTA_OK) return _s;    \
+    } while (0)
+// a gradient-scale pair that could not be produced (pairs used up, or the launch failed) must
+// not reach a kernel as a NULL scale pointer
+#define CHECK_PTR(p)                                  \
+    do {                                              \
+        if ((p) == nullptr) return CISTA_ERR_HIP;     \
     } while (0)
 
 bool overlaps(const void *a, size_t na, const void *b, size_t nb) {
@@ -1138,6 +1144,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // upsample conv wgrad as a stride-1 wgrad over the materialised up(h) (in dxpF, which
         // the dgrad below overwrites); the gradient scale is shared with that dgrad
         const float *gsu = scale_of(k);
+        CHECK_PTR(gsu);
         hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
         CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
@@ -1157,6 +1164,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     hipLaunchKernelGGL(lstm_bwd_kernel, g1d(hw * C), dim3(256), 0, st, (const float *)sv.lg, (const float *)io.c,
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C, scale_slots(k));
     const float *gsc = scale_of(k);
+    CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
     CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
@@ -1164,6 +1172,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
     gsc = scale_of(k);
+    CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
     CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
@@ -1193,10 +1202,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
         // P: v = z_k + P(x_k) + b_P
         gsc = scale_of(k, sclP + 2 * it);
+        CHECK_PTR(gsc);
         CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, C, 0, gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));   // gx1 += too
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
         gsc = scale_of(k, sclD + 2 * it);
+        CHECK_PTR(gsc);
         CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, gv));   // identity path + fold
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
@@ -1223,6 +1234,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C, scale_slots(k, 0), scale_slots(k, 1));
     gsc = scale_of(k);                                   // Go; Gl's scale is the next slot set
+    CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
@@ -1232,6 +1244,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
     gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
+    CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
@@ -1239,12 +1252,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
     if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
+    CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
     CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
     CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
     const float *gsx = scale_of(k);                     // gx1 is final: W0's output gradient
-    if (!gsx) return CISTA_ERR_HIP;
+    CHECK_PTR(gsx);
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
     float *xfull = ws.gU, *gxfull = ws.gU;   // x_full is dead once W0's wgrad has run
     {

@@ -164,7 +164,7 @@ struct ConvArgs {
     //   4*Cout channels in the reference gate order; EPI_UP_Q: out1 = u = relu(acc + b)
     float *out2;
     const float *ascale; // optional [2]: {s, 1/s} power-of-two input pre-scale (dgrad inputs)
-    int lds_flag;        // 4-byte LDS index of 8 words of range-pass scratch, outside the epilogue's
+    int lds_flag;        // 4-byte LDS index of 3 x waves words of range-pass scratch, outside the epilogue's
                          // LDS (the host sizes the allocation for it)
     int border;          // 0, or the border-strip tiling (see the kernel's tile origin)
     // STAGE_S2D: in0 = events (B, s2d_nb, 2Hin, 2Win), s2d_img = prev image (B, 1, 2Hin, 2Win)
@@ -523,10 +523,12 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
 }
 
 // Range pass, rare path (see conv3x3_split3): some staged value of this tile did not fit the
-// fp16 hi part.  The tile scans its inputs for max |x| (every K-chunk), takes the power of two s
-// with max |x s| <= 16384, and recomputes its accumulators from scratch on the same split-f16
-// MFMAs with every staged value pre-scaled by s (exact); the epilogue divides s out.  Accuracy is
-// the split path's relative to the tile's largest input.  A plain single-buffered K loop (one
+// fp16 hi part.  The tile scans its inputs for max |x| and min nonzero |x| (every K-chunk), takes
+// the power of two s_0 with max |x s_0| <= 16384, and recomputes its accumulators from scratch
+// on the same split-f16 MFMAs with every staged value pre-scaled (exact); the epilogue divides
+// s_0 out.  Values far below the tile max get their own larger scale (magnitude classes, one K
+// loop each), so that an O(1) value beside a 1e6 or 1e12 outlier keeps the split path's
+// relative accuracy instead of sinking into the fp16 subnormals.  A plain single-buffered K loop (one
 // LDS image, no prefetch) that recomputes every address per tap, so that nothing is held across
 // it: ~60 VGPRs beside the accumulators, which keeps the main loop's allocation (a second trip
 // through the main loop spilled 15-45 VGPRs in the 256-VGPR convs).  An fp32-MFMA re-run
@@ -573,7 +575,7 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
         segC = kc < kc0 ? a.c0 : a.c1;
         choff = (kc < kc0 ? kc : kc - kc0) * 32;
     };
-    float mx = 0.0f;
+    float mx = 0.0f, mn = 3.4e38f;                      // max |x|, min nonzero |x| of the tile
     for (int kc = 0; kc < nchunks; ++kc) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
@@ -583,24 +585,61 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
             float4 v0, v1;
             rare_item<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, (it >> 3) & 3, v0, v1);
             mx = fmaxf(mx, absmax8(v0, v1));
+            const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float av = fabsf(vv[i]);
+                mn = av > 0.0f ? fminf(mn, av) : mn;
+            }
         }
     }
-    for (int o = 32; o > 0; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o));
+    for (int o = 32; o > 0; o >>= 1) {
+        mx = fmaxf(mx, __shfl_xor(mx, o));
+        mn = fminf(mn, __shfl_xor(mn, o));
+    }
     float *flm = reinterpret_cast<float *>(smem) + a.lds_flag + NWV;
-    if (lane == 0) flm[wave] = mx;
+    if (lane == 0) {
+        flm[wave] = mx;
+        flm[NWV + wave] = mn;
+    }
     __syncthreads();
     mx = flm[0];
+    mn = flm[NWV];
 #pragma unroll
-    for (int w = 1; w < NWV; ++w) mx = fmaxf(mx, flm[w]);
+    for (int w = 1; w < NWV; ++w) {
+        mx = fmaxf(mx, flm[w]);
+        mn = fminf(mn, flm[NWV + w]);
+    }
     if (!(mx < 3.0e38f)) return 1.0f;                   // an inf input: the reference gives inf / NaN too
-    int e = (int)floorf(log2f(16384.0f / mx));
-    e = e < -126 ? -126 : (e > 0 ? 0 : e);
-    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ldexpf(1.0f, e))));
+    // Magnitude classes.  One power-of-two scale for the whole tile would push its small values
+    // into the fp16 subnormals (a 1e-3 beside a 1e6 outlier keeps ~2e-3 relative, a 1 beside a
+    // 1e12 nothing at all).  Class k takes the values with |x s_k| in [2^-5, 2^14], s_k =
+    // 2^(e0 + 19 k), where hi + lo holds them to ~2^-21 relative like the main path's O(1) values;
+    // up to 4 classes (76 binades below the tile max).  The classes run smallest first into the
+    // same accumulators, which are rescaled by s_{k-1} / s_k = 2^-19 (exact) before each larger
+    // class, so that they end in scale s_0 for the epilogue.
+    int e0 = (int)floorf(log2f(16384.0f / mx));
+    e0 = e0 < -126 ? -126 : (e0 > 0 ? 0 : e0);
+    int ncls = 1;
+    while (ncls < 4 && e0 + 19 * ncls <= 100 && ldexpf(0.03125f, -(e0 + 19 * (ncls - 1))) > mn) ++ncls;
+    ncls = __builtin_amdgcn_readfirstlane(ncls);
 #pragma unroll
     for (int m = 0; m < MT_W; ++m)
 #pragma unroll
         for (int n = 0; n < NW; ++n) acc[m][n] = f32x4{0.f, 0.f, 0.f, 0.f};
     f16x2 unused = {};
+    for (int cls = ncls - 1; cls >= 0; --cls) {
+    const int ek = e0 + 19 * cls;
+    const float s = __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ldexpf(1.0f, ek))));
+    // |x| in [lower, upper) belongs to this class (upper = inf for class 0, lower = 0 for the last)
+    const float lower = cls == ncls - 1 ? 0.0f : ldexpf(0.03125f, -ek);
+    const float upper = cls == 0 ? __builtin_huge_valf() : ldexpf(0.03125f, -(ek - 19));
+    if (cls != ncls - 1) {
+#pragma unroll
+        for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+            for (int n = 0; n < NW; ++n) acc[m][n] *= 1.9073486328125e-06f;   // 2^-19
+    }
     for (int kc = 0; kc < nchunks; ++kc) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
@@ -610,8 +649,16 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
             if (hp >= HP) continue;
             float4 v0, v1;
             rare_item<STAGE>(a, b, iy0, ix0, HWd, seg, segC, choff, hp, g, v0, v1);
-            v0.x *= s; v0.y *= s; v0.z *= s; v0.w *= s;
-            v1.x *= s; v1.y *= s; v1.z *= s; v1.w *= s;
+            float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const float av = fabsf(vv[i]);
+                // NaN is kept in class 0 (it must reach the output like torch's)
+                const bool in = (av >= lower && av < upper) || (cls == 0 && av != av);
+                vv[i] = in ? vv[i] * s : 0.0f;
+            }
+            v0 = make_float4(vv[0], vv[1], vv[2], vv[3]);
+            v1 = make_float4(vv[4], vv[5], vv[6], vv[7]);
             u32x4 hi, lo;
             split8(v0, v1, hi, lo, unused);
             smem[g * HPpad + hp] = hi;
@@ -641,8 +688,9 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
             mfma_tap<MT_W, NW>(acc, smem, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh, bl);
         }
     }
+    }
     __syncthreads();                                    // the epilogue may reuse the LDS
-    return s;
+    return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ldexpf(1.0f, e0))));
 }
 
 // ------------------------------------------------------------------------------------------

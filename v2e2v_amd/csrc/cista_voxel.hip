@@ -58,28 +58,64 @@ __device__ __forceinline__ int window_of(const long long *off, int B, long long 
     return lo;
 }
 
-// Reference :53-58: np.add.at on the flat index x + y W + bin H W raises IndexError when an index
-// reaches the grid size, and otherwise adds an event outside the H x W frame to another pixel (or
-// bin).  Such an event is dropped here; this records which of the two the reference does with it:
-// CISTA_VOXEL_OUT_OF_RANGE (it raises) or CISTA_VOXEL_SPILL (it writes elsewhere).  Called for the
-// events outside the frame only (rare).  x, y as np.uint: truncated toward zero and wrapped
-// modulo 2^64 (float -3.0 -> 2^64 - 3), and np.add.at reads the uint64 index as intp, so the sum
-// is a signed index: in [-size, size) it is valid (a negative one counts from the end of the
-// grid, Python-style), outside it raises.
-__device__ __noinline__ void grid_status(const double *e, double x, double y, double first, double dT, int nb,
-                                         int H, int W, bool torch_floor, int *status) {
+// Events outside the H x W frame (x >= W, y >= H, or negative).  Reference :53-58: np.add.at on
+// the flat index x + y W + bin H W raises IndexError when an index leaves the grid, and otherwise
+// adds the event to another cell: x >= W moves it down a row, y >= H to a later bin, a negative x
+// back a row.  x, y as np.uint are truncated toward zero and wrapped modulo 2^64 (float -3.0 ->
+// 2^64 - 3), and np.add.at reads the uint64 index as intp, so the sum is a signed index: in
+// [-size, size) it is valid (a negative one counts from the end of the grid, Python-style),
+// outside it raises.  The torch twin (:113-124, int64 index_add_) raises on negative indices too.
+// flat_cell: the grid index (normalised into [0, size)) of contribution `bin` of such an event, or
+// -1 where the reference raises.
+__device__ __forceinline__ long long flat_cell(double x, double y, long long bin, int nb, int H, int W, bool torch_idx) {
+    const long long HW = (long long)H * W, size = (long long)nb * HW;
+    if (!(fabs(x) < 1.0e15) || !(fabs(y) < 1.0e15)) return -1;             // NaN / inf included
+    const long long i = (long long)x + (long long)y * W + bin * HW;        // trunc, signed
+    if (i >= size || i < (torch_idx ? 0 : -size)) return -1;
+    return i < 0 ? i + size : i;
+}
+
+// Classifies one out-of-frame event (rare path): ORs CISTA_VOXEL_OUT_OF_RANGE (the reference
+// raises) or CISTA_VOXEL_SPILL (it adds the event elsewhere) into *status, and returns the pixel
+// (in [0, HW)) its contributions land on -- both share it: the right one is the left one plus
+// H W, modulo the grid -- or -1 when it hits no bin or the reference raises.  Such an event is
+// then sorted and accumulated with that pixel's own events, in event order, its bins taken from
+// flat_cell (spill_bins), so the grid is bit-identical to np.add.at's.
+__device__ __noinline__ long long grid_status(const double *e, double x, double y, double first, double dT, int nb,
+                                              int H, int W, bool torch_floor, int *status) {
     const double ts = (double)(nb - 1) * (e[0] - first) / dT;
     const double tf = torch_floor ? floor(ts) : ts;
-    if (!(tf > -1.0) || !(tf < 9.0e18) || (torch_floor && tf < 0.0)) return;   // hits no bin
+    if (!(tf > -1.0) || !(tf < 9.0e18) || (torch_floor && tf < 0.0)) return -1;   // hits no bin
     const long long ti = (long long)tf;
-    const long long HW = (long long)H * W, size = (long long)nb * HW;
-    const bool huge = !(fabs(x) < 1.0e15) || !(fabs(y) < 1.0e15);            // NaN / inf included
-    const long long flat = huge ? 0 : (long long)x + (long long)y * W;      // trunc, signed
-    auto bad = [&](long long i) { return huge || i < -size || i >= size; };
+    const long long HW = (long long)H * W;
     int f = 0;
-    if (ti < nb) f |= bad(flat + ti * HW) ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
-    if (ti + 1 < nb) f |= bad(flat + (ti + 1) * HW) ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
-    if (f) atomicOr(status, f);
+    long long cl = -1, cr = -1;
+    if (ti < nb) {
+        cl = flat_cell(x, y, ti, nb, H, W, torch_floor);
+        f |= cl < 0 ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
+    }
+    if (ti + 1 < nb) {
+        cr = flat_cell(x, y, ti + 1, nb, H, W, torch_floor);
+        f |= cr < 0 ? CISTA_VOXEL_OUT_OF_RANGE : CISTA_VOXEL_SPILL;
+    }
+    if (f && status) atomicOr(status, f);
+    if (f == 0 || (f & CISTA_VOXEL_OUT_OF_RANGE)) return -1;
+    return cl % HW;                                  // ti + 1 < nb implies ti < nb: cl is set
+}
+
+// bins of the left / right contribution of an event with time bin ti: (ti, ti + 1) inside the
+// frame; for an out-of-frame event the bins of its flat cells (its pixel is its sort key)
+__device__ __forceinline__ void spill_bins(double x, double y, unsigned long long ti, int nb, int H, int W,
+                                           bool torch_idx, unsigned long long &bl, unsigned long long &br) {
+    bl = ti;
+    br = ti + 1;
+    if (x > -1.0 && x < (double)W && y > -1.0 && y < (double)H) return;
+    const long long HW = (long long)H * W;
+    const long long cl = ti < (unsigned long long)nb ? flat_cell(x, y, (long long)ti, nb, H, W, torch_idx) : -1;
+    const long long cr = ti + 1 < (unsigned long long)nb ? flat_cell(x, y, (long long)ti + 1, nb, H, W, torch_idx) : -1;
+    // an invalid cell (the reference raised: reported by grid_status) gets bin nb, i.e. none
+    bl = cl < 0 ? (unsigned long long)nb : (unsigned long long)(cl / HW);
+    br = cr < 0 ? (unsigned long long)nb : (unsigned long long)(cr / HW);
 }
 
 __global__ void vox_keys_kernel(const double *ev, const long long *off, int B, long long N, int H, int W,
@@ -91,13 +127,14 @@ __global__ void vox_keys_kernel(const double *ev, const long long *off, int B, l
     const unsigned long long HW = (unsigned long long)H * W;
     unsigned long long key = (unsigned long long)B * HW;   // sentinel: sorts last, ignored
     // reference :42-43: astype(np.uint) truncates toward zero, so (-1, W) maps into [0, W)
-    if (x > -1.0 && x < (double)W && y > -1.0 && y < (double)H)
+    if (x > -1.0 && x < (double)W && y > -1.0 && y < (double)H) {
         key = (unsigned long long)b * HW + (unsigned long long)y * W + (unsigned long long)x;
-    else if (status) {
+    } else {                                  // rare: the pixel the reference's flat index hits
         const long long e0 = off[b], e1 = off[b + 1] - 1;
         double dT = ev[4 * e1] - ev[4 * e0];
         if (dT == 0.0) dT = 1.0;
-        grid_status(ev + 4 * i, x, y, ev[4 * e0], dT, nb, H, W, torch_acc != 0, status);
+        const long long p = grid_status(ev + 4 * i, x, y, ev[4 * e0], dT, nb, H, W, torch_acc != 0, status);
+        if (p >= 0) key = (unsigned long long)b * HW + (unsigned long long)p;
     }
     keys[i] = key;
     vals[i] = (int)i;
@@ -156,37 +193,36 @@ __global__ void vox_accum_kernel(const unsigned long long *keys, const int *vals
     float *out = vox + (size_t)b * nb * HW + p;
     long long end = j;
     while (end < N && keys[end] == key) ++end;
+    // an out-of-frame event grouped here (its flat index hits pixel p) adds to the bins of its
+    // flat cells (spill_bins); in-frame events to (ti, ti + 1)
     if (torch_acc) {                    // index_add_ #1 / #2 (:112-127), float32 adds
-        for (long long k = j; k < end; ++k) {
-            EvValT v;
-            if (event_value_torch(ev + 4 * (long long)vals[k], first, dT, nb, v) && v.ti < (unsigned long long)nb)
-                out[v.ti * HW] += v.vl;
-        }
-        for (long long k = j; k < end; ++k) {
-            EvValT v;
-            if (event_value_torch(ev + 4 * (long long)vals[k], first, dT, nb, v) && v.ti + 1 < (unsigned long long)nb)
-                out[(v.ti + 1) * HW] += v.vr;
-        }
+        for (int ph = 0; ph < 2; ++ph)
+            for (long long k = j; k < end; ++k) {
+                const double *e = ev + 4 * (long long)vals[k];
+                EvValT v;
+                if (!event_value_torch(e, first, dT, nb, v)) continue;
+                unsigned long long bl, br;
+                spill_bins(e[1], e[2], v.ti, nb, H, W, true, bl, br);
+                const unsigned long long bin = ph ? br : bl;
+                if (bin < (unsigned long long)nb) out[bin * HW] += ph ? v.vr : v.vl;
+            }
         return;
     }
-    // np.add.at #1 (:53-54): left contributions of the whole window, in event order
-    for (long long k = j; k < end; ++k) {
-        EvVal v;
-        if (!event_value(ev + 4 * (long long)vals[k], first, dT, nb, v)) continue;
-        if (v.ti < (unsigned long long)nb) {
-            float *d = out + v.ti * HW;
-            *d = (float)((double)*d + v.vl);
-        }
-    }
+    // np.add.at #1 (:53-54): left contributions of the whole window, in event order; then
     // np.add.at #2 (:56-58): right contributions
-    for (long long k = j; k < end; ++k) {
-        EvVal v;
-        if (!event_value(ev + 4 * (long long)vals[k], first, dT, nb, v)) continue;
-        if (v.ti + 1 < (unsigned long long)nb) {
-            float *d = out + (v.ti + 1) * HW;
-            *d = (float)((double)*d + v.vr);
+    for (int ph = 0; ph < 2; ++ph)
+        for (long long k = j; k < end; ++k) {
+            const double *e = ev + 4 * (long long)vals[k];
+            EvVal v;
+            if (!event_value(e, first, dT, nb, v)) continue;
+            unsigned long long bl, br;
+            spill_bins(e[1], e[2], v.ti, nb, H, W, false, bl, br);
+            const unsigned long long bin = ph ? br : bl;
+            if (bin < (unsigned long long)nb) {
+                float *d = out + bin * HW;
+                *d = (float)((double)*d + (ph ? v.vr : v.vl));
+            }
         }
-    }
 }
 
 // ------------------------------------------------------------------------------------------
@@ -237,10 +273,11 @@ __device__ __forceinline__ int key_lower(const unsigned *k, int n, unsigned p) {
 // segments at its event offsets); tb: TBMAX + 1 tile starts per window (single-segment windows)
 __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const long long *off, int nb, int H, int W,
                                                       int end_bit, unsigned *scratch, double2 *tp_sorted, int *tb,
-                                                      int torch_acc, int *status) {
+                                                      int *spw, int torch_acc, int *status) {
     extern __shared__ __align__(16) char wsm[];
     WinLds &L = *reinterpret_cast<WinLds *>(wsm);
     const int b = blockIdx.x, tid = threadIdx.x;
+    int spill = 0;                      // this thread keyed an out-of-frame event to a pixel
     const long long e0 = off[b];
     const int n = (int)(off[b + 1] - e0);
     const int nseg = (n + WSEG - 1) / WSEG;
@@ -267,10 +304,15 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
                 // reference :42-43: astype(np.uint) truncates toward zero
                 const bool in = l < cnt && x[i] > -1.0 && x[i] < (double)W && y[i] > -1.0 && y[i] < (double)H;
                 key[i0 + i] = in ? ((((unsigned)y[i] * (unsigned)W + (unsigned)x[i]) << 14) | (unsigned)l) : 0xFFFFFFFFu;
-                if (__builtin_expect(status && l < cnt && !in, 0)) {
+                if (__builtin_expect(l < cnt && !in, 0)) {      // rare: keyed to the pixel it spills to
                     double dT = ev[4 * (e0 + n - 1)] - ev[4 * e0];
                     if (dT == 0.0) dT = 1.0;
-                    grid_status(ev + 4 * (base + l), x[i], y[i], ev[4 * e0], dT, nb, H, W, torch_acc != 0, status);
+                    const long long p = grid_status(ev + 4 * (base + l), x[i], y[i], ev[4 * e0], dT, nb, H, W,
+                                                    torch_acc != 0, status);
+                    if (p >= 0) {
+                        key[i0 + i] = ((unsigned)p << 14) | (unsigned)l;
+                        spill = 1;
+                    }
                 }
             }
         }
@@ -307,6 +349,8 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
             if (l < cnt) scratch[base + l] = key[i];
         }
     }
+    spill = __syncthreads_or(spill);
+    if (tid == 0) spw[b] = spill;
     if (nseg == 1) {
         __syncthreads();
         const unsigned HW = (unsigned)H * (unsigned)W;
@@ -319,9 +363,12 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
 // ---- group walks of the tile kernel; cell (bin, pixel p) = tile[bin * TP + p - pa] ----
 // General walk (RMW on the LDS cells): sorted positions [s, e) of one segment; pass 1 = left
 // contributions, 2 = right, 3 = both (in that order: single-segment windows)
+// evs: the segment's event rows (window with spilled events: evs != nullptr, every event's bins
+// through spill_bins from its own x, y; the key's low 14 bits index the row)
 template <bool TORCH>
 __device__ void walk_groups(const unsigned *k, int s, int e, const double2 *tps, double first, double dT, int nb,
-                            float *tile, int TP, unsigned pa, int pass) {
+                            float *tile, int TP, unsigned pa, int pass, const double *evs = nullptr, int H = 0,
+                            int W = 0) {
     for (int j = s + (int)threadIdx.x; j < e; j += TT) {
         const unsigned p = k[j] >> 14;
         if (j > s && (k[j - 1] >> 14) == p) continue;                   // not the group head
@@ -333,15 +380,31 @@ __device__ void walk_groups(const unsigned *k, int s, int e, const double2 *tps,
             for (int q = j; q < g; ++q) {
                 const double2 r = tps[q];
                 const double ev[4] = {r.x, 0.0, 0.0, r.y};
+                double ex = 0.0, ey = 0.0;
+                if (evs) {
+                    const double *row = evs + 4 * (long long)(k[q] & 0x3FFFu);
+                    ex = row[1];
+                    ey = row[2];
+                }
                 if (TORCH) {
                     EvValT v;
                     if (!event_value_torch(ev, first, dT, nb, v)) continue;
-                    const unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    if (evs) {
+                        unsigned long long bl, br;
+                        spill_bins(ex, ey, v.ti, nb, H, W, true, bl, br);
+                        bin = ph == 2 ? br : bl;
+                    }
                     if (bin < (unsigned long long)nb) cell[bin * TP] += ph == 1 ? v.vl : v.vr;
                 } else {
                     EvVal v;
                     if (!event_value(ev, first, dT, nb, v)) continue;
-                    const unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    unsigned long long bin = v.ti + (ph == 2 ? 1 : 0);
+                    if (evs) {
+                        unsigned long long bl, br;
+                        spill_bins(ex, ey, v.ti, nb, H, W, false, bl, br);
+                        bin = ph == 2 ? br : bl;
+                    }
                     if (bin < (unsigned long long)nb) {
                         float *d = cell + bin * TP;
                         *d = (float)((double)*d + (ph == 1 ? v.vl : v.vr));
@@ -441,7 +504,7 @@ __device__ void walk_fast(const unsigned *k, int e, const double2 *tps, double f
 template <bool TORCH>
 __global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const long long *off, int nb, int H, int W,
                                                       const unsigned *scratch, const double2 *tps, const int *tb,
-                                                      float *vox) {
+                                                      const int *spw, float *vox) {
     __shared__ __align__(16) float tile[WTILE];
     __shared__ int rng[2];
     const int t = blockIdx.x, b = blockIdx.y, tid = threadIdx.x;
@@ -464,7 +527,9 @@ __global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const lo
     } else if (nseg == 1) {
         const int *tbw = tb + (size_t)b * (TBMAX + 1);
         const int s = tbw[t], e = tbw[t + 1];
-        if (nb <= WNB) {
+        if (spw[b]) {                      // rare: events spilled into this window's grid
+            walk_groups<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa, 3, ev + 4 * e0, H, W);
+        } else if (nb <= WNB) {
             walk_fast<TORCH>(scratch + e0 + s, e - s, tps + e0 + s, first, dT, nb, tile, TP, pa);
         } else {
             walk_groups<TORCH>(scratch + e0, s, e, tps + e0, first, dT, nb, tile, TP, pa, 3);
@@ -479,7 +544,8 @@ __global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const lo
                     rng[1] = key_lower(scratch + base, cnt, pa + np);
                 }
                 __syncthreads();
-                walk_groups<TORCH>(scratch + base, rng[0], rng[1], tps + base, first, dT, nb, tile, TP, pa, pass);
+                walk_groups<TORCH>(scratch + base, rng[0], rng[1], tps + base, first, dT, nb, tile, TP, pa, pass,
+                                   spw[b] ? ev + 4 * base : nullptr, H, W);
                 __syncthreads();
             }
     }
@@ -895,6 +961,7 @@ struct VoxWs {
     unsigned long long *k0, *k1;
     int *v0, *v1;
     int *tb;                 // per-window tile starts of the sort + tile path
+    int *spw;                // per-window flag of the same path: out-of-frame events spill into the grid
     void *tps;               // (t, polarity) of every event in sorted order (same path)
     ChunkPart *parts;
     Part64 *parts64;         // CISTA_VOXEL_STD_F32 block partials
@@ -927,6 +994,7 @@ VoxWs carve(void *base, int B, long long N, int nb, int H, int W) {
     w.v1 = static_cast<int *>(take(NN * 4));
     w.tb = static_cast<int *>(take((size_t)(B > 0 ? B : 1) * (TBMAX + 1) * 4));
     w.tps = take(NN * 16);
+    w.spw = static_cast<int *>(take((size_t)(B > 0 ? B : 1) * 4));
     w.parts = static_cast<ChunkPart *>(take((size_t)(B > 0 ? B : 1) * nchunks * sizeof(ChunkPart)));
     w.stats = static_cast<WinStats *>(take((size_t)(B > 0 ? B : 1) * sizeof(WinStats)));
     w.parts64 = static_cast<Part64 *>(take((size_t)(B > 0 ? B : 1) * nblk64(n) * sizeof(Part64)));
@@ -1021,10 +1089,10 @@ int cista_voxelize_checked(const double *events, const long long *offsets, int B
         int *tb = reinterpret_cast<int *>(w.tb);
         double2 *tps = reinterpret_cast<double2 *>(w.tps);
         hipLaunchKernelGGL(vox_sort_kernel, dim3(B), dim3(WT), sizeof(WinLds), st, events, offsets, num_bins, height,
-                           width, 14 + end_bits(HW), scr, tps, tb, torch_acc, grid_status);
+                           width, 14 + end_bits(HW), scr, tps, tb, w.spw, torch_acc, grid_status);
         hipLaunchKernelGGL(torch_acc ? vox_tile_kernel<true> : vox_tile_kernel<false>, dim3(ntiles, B), dim3(TT), 0,
                            st, events, offsets, num_bins, height, width, (const unsigned *)scr, (const double2 *)tps,
-                           (const int *)tb, voxels);
+                           (const int *)tb, (const int *)w.spw, voxels);
         if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
         return preprocess(voxels, B, n, mode, hot_threshold, w, st);
     }

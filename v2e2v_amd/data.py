@@ -249,11 +249,18 @@ class GpuVoxelLoader:
         self.ds = dataset
         self.device = torch.device(device)
         self.strict = bool(strict)
+        dd = torch.distributed
+        pg = dd.is_available() and dd.is_initialized()
         if world_size is None:
-            dd = torch.distributed
-            world_size = dd.get_world_size() if dd.is_available() and dd.is_initialized() else 1
-            rank = dd.get_rank() if world_size > 1 else 0
-        self.rank, self.world_size = int(rank or 0), int(world_size)
+            world_size = dd.get_world_size() if pg else 1
+        if rank is None:
+            if int(world_size) > 1 and not pg:
+                # every process would otherwise take rank 0 and read the same shard
+                raise ValueError("GpuVoxelLoader: world_size > 1 needs rank= (or an initialised process group)")
+            rank = dd.get_rank() if int(world_size) > 1 else 0
+        if not 0 <= int(rank) < int(world_size):
+            raise ValueError(f"GpuVoxelLoader: rank {rank} outside world_size {world_size}")
+        self.rank, self.world_size = int(rank), int(world_size)
         self.sampler = None
         if self.world_size > 1:
             if "sampler" in loader_kwargs or loader_kwargs.get("shuffle"):

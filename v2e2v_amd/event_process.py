@@ -15,15 +15,16 @@ twins are bit-identical to the reference's numpy path (voxel accumulation order,
 pairwise reduction for the 'std' statistics); the torch twins follow the reference's torch
 arithmetic: events_to_voxel_grid_pytorch bit-identically (float32 contributions, float32
 index_add_), event_preprocess_pytorch with float32 statistics (its sum() rounded once: ATen's
-reduction order may differ in the last bit, tests/test_gpu_voxel.py bounds it at 2e-6).  Differences from the reference, by design:
-inputs are never modified (the reference rewrites ``events[:, 0]``, the polarity column, and the
-voxel grid when filtering hot pixels), and events outside the grid are dropped instead of raising
-IndexError.  There is no CPU fallback: without the HIP library every call raises.
+reduction order may differ in the last bit, tests/test_gpu_voxel.py bounds it at 2e-6).  Events
+outside the H x W frame are treated as the reference's flat index treats them: added to the
+pixel / bin it lands on (bit-identically, in event order with that cell's own events), or
+IndexError where the reference raises.  Difference from the reference, by design: inputs are
+never modified (the reference rewrites ``events[:, 0]``, the polarity column, and the voxel grid
+when filtering hot pixels).  There is no CPU fallback: without the HIP library every call raises.
 """
 from __future__ import annotations
 
 import ctypes
-import warnings
 
 import numpy as np
 import torch
@@ -78,12 +79,12 @@ def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode:
     ``filter_hot_pixel`` uses the numpy threshold 25/num_bins unless ``hot_threshold`` is given.
     ``torch_semantics``: the torch twins' arithmetic (events_to_voxel_grid_pytorch accumulation,
     event_preprocess_pytorch float32 'std' statistics) instead of the numpy path's.
-    ``strict`` (default): events outside the H x W frame are checked the way the reference's
-    ``np.add.at`` on the flat index treats them (utils/event_process.py:53-58): an index past the
-    grid raises IndexError as there; an event the reference would add to another pixel or bin
-    (x >= W or y >= H at a flat index inside the grid) is dropped here and reported with a
-    RuntimeWarning.  Costs one stream synchronisation; ``strict=False`` skips it (such events are
-    dropped silently).
+    Events outside the H x W frame go where the reference's flat index x + y*W + bin*H*W puts them
+    (utils/event_process.py:53-58 ``np.add.at``, :113-124 ``index_add_``): an event the reference
+    adds to another pixel or bin (x >= W, y >= H or a negative x, at an index inside the grid) is
+    added there, bit-identically.  ``strict`` (default): an index the reference rejects raises
+    IndexError as there (one stream synchronisation); ``strict=False`` skips the check and drops
+    such events.
     Returns (B, num_bins, height, width) float32 on the GPU.
     """
     if num_bins <= 0 or width <= 0 or height <= 0:
@@ -123,10 +124,6 @@ def events_to_voxel_batch(windows, num_bins: int, width: int, height: int, mode:
             raise IndexError(f"index out of bounds for a voxel grid of size {num_bins * height * width}: an event's "
                              f"x, y lie outside the {height}x{width} frame (np.add.at raises here, "
                              "utils/event_process.py:53-58)")
-        if flags & SPILL:
-            warnings.warn(f"events outside the {height}x{width} frame were dropped; the reference adds them "
-                          "to another pixel or bin (np.add.at on the flat index x + y*W + bin*H*W)",
-                          RuntimeWarning, stacklevel=2)
     return out
 
 

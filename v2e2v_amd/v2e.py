@@ -244,6 +244,8 @@ class EventEmulator(torch.nn.Module):
         self.num_events = int(n.value)
         if loops.value == 0:                          # no iteration ran: torch.tensor([]) (:347)
             return torch.zeros(0, device=fr.device), self.num_events
+        if self._rows is None:                        # iterations ran, but every event was filtered out
+            return torch.zeros(0, 5, device=fr.device), self.num_events
         return self._rows[:self.num_events].clone(), self.num_events
 
 
