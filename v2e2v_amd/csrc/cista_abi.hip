@@ -775,6 +775,7 @@ constexpr int SCL_PAIRS = 16;                // scale pairs of the non-ISTA grad
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *gx1, *Go, *gz0;
+    float *fb;          // border lines of an EPI_FOLD dgrad's padded output (fold_border_index)
     float *part, *bpart, *dlp;
     float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
     unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses)
@@ -809,6 +810,10 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.gx1 = take(hw * C);
     s.Go = take(hw * 2 * C);
     s.gz0 = take(hw * 2 * C);
+    {
+        const size_t lh = (size_t)B * (2 * (w + 2) + 2 * h) * 4 * C, lf = (size_t)B * (2 * (W + 2) + 2 * H) * C;
+        s.fb = take(lh > lf ? lh : lf);
+    }
     s.part = take((size_t)WG_BLOCKS * 32 * 32 * 9);
     s.bpart = take((size_t)WG_BLOCKS * 4 * C);
     s.dlp = take((size_t)2 * C * 512);
@@ -1096,6 +1101,43 @@ int dgrad_conv(Bwd &k, int id, const float *G, float *dxp, const float *sc = nul
     return launch_conv<STAGE_ZP2, EPI_BIAS, 1>(a, k.st);
 }
 
+#ifndef CISTA_FOLD_EPI
+#define CISTA_FOLD_EPI 1   // dgrads fold the reflect padding in their epilogue (0: fold_reflect_kernel pass)
+#endif
+
+FoldSeg fseg(float *dst, int Cd, int dc0, float scale = 1.0f, int mode = FOLD_SET, float *aux = nullptr,
+             unsigned *amax = nullptr) {
+    FoldSeg f;
+    f.dst = dst; f.aux = aux; f.Cd = Cd; f.dc0 = dc0; f.mode = mode; f.scale = scale; f.amax = amax;
+    return f;
+}
+
+// input gradient of conv `id` from G (B, Hin, Win, K) with the reflect fold in the conv epilogue:
+// packed columns [0, split) -> s0, [split, N) -> s1 (FoldSeg), then fold_fix_kernel for the
+// reflected border terms.  sc: grad_scale of G.
+int dgrad_fold(Bwd &k, int id, const float *G, const float *sc, const FoldSeg &s0, const FoldSeg &s1, int split) {
+    const ConvShape s = conv_shape(id, k.C);
+    const int Hin = id == CV_UP ? k.H : k.h, Win = id == CV_UP ? k.W : k.w;
+    if (Hin < 4 || Win < 4 || split % 16) return CISTA_ERR_UNSUPPORTED;
+    ConvArgs a;
+    memset(&a, 0, sizeof(a));
+    a.in0 = G; a.c0 = s.cout; a.in1 = nullptr; a.c1 = 0;
+    a.B = k.B; a.Hin = Hin; a.Win = Win; a.Hout = Hin + 2; a.Wout = Win + 2;
+    a.wpack = blob<u32x4>(k.packed, k.L.dwp[id]);
+    a.bias = blob<float>(k.packed, k.L.dbp[id]);
+    a.wscale = blob<float>(k.packed, k.L.sc[id]) + 1;
+    a.ascale = sc;
+    a.N = s.cin; a.Cout = s.cin;
+    a.fseg[0] = s0; a.fseg[1] = s1; a.fsplit = split;
+    a.fborder = k.ws.fb;
+    CHECK((launch_conv<STAGE_ZP2, EPI_FOLD, 1>(a, k.st)));
+    FoldFixArgs f;
+    f.fb = k.ws.fb; f.N = s.cin; f.B = k.B; f.n = Hin; f.m = Win;
+    f.seg[0] = s0; f.seg[1] = s1; f.fsplit = split;
+    hipLaunchKernelGGL(fold_fix_kernel, g1d((long)k.B * (2 * Win + 2 * (Hin - 2)) * (s.cin / 4)), dim3(256), 0, k.st, f);
+    return hip_ok();
+}
+
 // add: dst = add + fold (copy-free identity path; NULL add with accumulate 0 is plain dst = fold);
 // dst2: a second destination receiving dst2 += fold from the same pass over src
 int fold(Bwd &k, const float *src, int Cs, int sc0, float *dst, int Cd, int dc0, int n, int H, int W,
@@ -1149,9 +1191,15 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
         CHECK(side_join(k));                            // dxpF (its X) is overwritten next
-        CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
-        CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));   // g wrt up(h)
-        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C / 4), dim3(256), 0, st, (const float *)ws.gU, ws.ghb,
+        float *gup = ws.gU;                              // g wrt up(h)
+        if (CISTA_FOLD_EPI) {
+            gup = ws.dxpF;                               // (B, H, W, C): the dgrad's input gU is still read
+            CHECK(dgrad_fold(k, CV_UP, ws.gU, gsu, fseg(gup, C, 0), fseg(nullptr, 0, 0), C));
+        } else {
+            CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
+            CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));
+        }
+        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C / 4), dim3(256), 0, st, (const float *)gup, ws.ghb,
                            B, h, w, C, 1);
     } else {
         if (hipMemsetAsync(pg.final_b, 0, 4, st) != hipSuccess ||
@@ -1167,16 +1215,26 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
-    CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y, nullptr, nullptr, scale_slots(k)));   // relu(Dg) mask
-    if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
+    if (CISTA_FOLD_EPI) {                                // relu(Dg) mask; h_prev's part if wanted
+        CHECK(dgrad_fold(k, CV_LSTM, ws.Gl, gsc, fseg(ws.gy, C, 0, 1.0f, FOLD_MASK, const_cast<float *>(sv.y), scale_slots(k)),
+                         fseg(io.h_prev ? g.g_h_prev : nullptr, C, 0), C));
+    } else {
+        CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y, nullptr, nullptr, scale_slots(k)));
+        if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
+    }
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
     gsc = scale_of(k);
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
-    CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr, g.g_z));   // g_z + fold
+    if (CISTA_FOLD_EPI) {                                // g_z + fold
+        CHECK(dgrad_fold(k, CV_DG, ws.gy, gsc, fseg(ws.gz, 2 * C, 0, 1.0f, g.g_z ? FOLD_ADD : FOLD_SET, const_cast<float *>(g.g_z)),
+                         fseg(nullptr, 0, 0), 2 * C));
+    } else {
+        CHECK(dgrad_conv(k, CV_DG, ws.gy, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr, g.g_z));
+    }
     // ---- 5. ISTA, reversed (tied D, P, lambda accumulate over iterations) -------------------
     const float *lam = blob<float>(k.packed, k.L.lambda);
     if (D == 0) {
@@ -1203,13 +1261,21 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // P: v = z_k + P(x_k) + b_P
         gsc = scale_of(k, sclP + 2 * it);
         CHECK_PTR(gsc);
-        CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, C, 0, gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));   // gx1 += too
+        if (CISTA_FOLD_EPI) {                            // gx1 += too
+            CHECK(dgrad_fold(k, CV_P, gv, gsc, fseg(gxk, C, 0, 1.0f, FOLD_DST2, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
+        } else {
+            CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
+            CHECK(fold(k, ws.dxp, C, 0, gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));
+        }
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
         gsc = scale_of(k, sclD + 2 * it);
         CHECK_PTR(gsc);
-        CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
-        CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, gv));   // identity path + fold
+        if (CISTA_FOLD_EPI) {                            // identity path + fold
+            CHECK(dgrad_fold(k, CV_D, gxk, gsc, fseg(ws.gz, 2 * C, 0, -1.0f, FOLD_ADD, gv), fseg(nullptr, 0, 0), 2 * C));
+        } else {
+            CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
+            CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, gv));
+        }
         // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
         hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
                            pg.lambda, it != D - 1);
@@ -1238,25 +1304,39 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
-    CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr, nullptr, nullptr,
-               scale_slots(k, 1)));                           // gz0 is final here: its slot set follows Gl's
     const bool want_zp = io.z_prev && g.g_z_prev;
-    if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
+    if (CISTA_FOLD_EPI) {                                // gz0 is final here: its slot set follows Gl's
+        CHECK(dgrad_fold(k, CV_OUTG, ws.Go, gsc, fseg(ws.gz0, 2 * C, 0, 1.0f, FOLD_ADD, ws.gz0, scale_slots(k, 1)),
+                         fseg(want_zp ? g.g_z_prev : nullptr, 2 * C, 0), 2 * C));
+    } else {
+        CHECK(dgrad_conv(k, CV_OUTG, ws.Go, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, 4 * C, 0, ws.gz0, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr, nullptr, nullptr,
+                   scale_slots(k, 1)));
+        if (want_zp) CHECK(fold(k, ws.dxp, 4 * C, 2 * C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 0, nullptr));
+    }
     gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
-    CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
-    if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    if (CISTA_FOLD_EPI) {
+        CHECK(dgrad_fold(k, CV_GATES, ws.Gl, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1),
+                         fseg(want_zp ? g.g_z_prev : nullptr, 2 * C, 0, 1.0f, FOLD_ADD, want_zp ? g.g_z_prev : nullptr), C));
+    } else {
+        CHECK(dgrad_conv(k, CV_GATES, ws.Gl, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, 3 * C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr));
+        if (want_zp) CHECK(fold(k, ws.dxp, 3 * C, C, g.g_z_prev, 2 * C, 0, 2 * C, h, w, 1.0f, 1, nullptr));
+    }
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
-    CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
-    CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
+    if (CISTA_FOLD_EPI) {
+        CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
+    } else {
+        CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
+        CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
+    }
     const float *gsx = scale_of(k);                     // gx1 is final: W0's output gradient
     CHECK_PTR(gsx);
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------

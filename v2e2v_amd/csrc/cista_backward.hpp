@@ -52,7 +52,7 @@ __device__ __forceinline__ int refl_sources(int i, int n, int (&out)[3]) {
 // separate 64-B lines, so no address sees more than ~1/256 of the workgroups.  slots_scale_kernel
 // turns the slots into {s, 1/s} and re-zeroes them.  (Replaces a separate absmax pass per
 // gradient tensor, 16 us each at B = 8.)
-constexpr int AMAX_SLOTS = 256, AMAX_STRIDE = 16;
+// (AMAX_SLOTS / AMAX_STRIDE / amax4f: cista_kernels.hpp)
 __device__ __forceinline__ void amax_publish(unsigned *slots, float m) {
     __shared__ float amax_red[4];
     __syncthreads();                            // a previous call's reads of amax_red are done
@@ -64,10 +64,6 @@ __device__ __forceinline__ void amax_publish(unsigned *slots, float m) {
         if (b > 0.0f) atomicMax(slots + (blockIdx.x & (AMAX_SLOTS - 1)) * AMAX_STRIDE, __float_as_uint(b));
     }
 }
-__device__ __forceinline__ float amax4f(float m, const float4 &v) {
-    return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
-}
-
 __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
     const int g4 = a.n / 4;
     const long total = (long)a.B * a.H * a.W * g4;
@@ -108,6 +104,79 @@ __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
     }
     if (live) *d = r;
     if (a.amax) amax_publish(a.amax, live ? amax4f(0.0f, r) : 0.0f);
+}
+
+// --------------------------------------------------------------------------------------------
+// The reflected terms of an EPI_FOLD dgrad (the conv epilogue wrote each input pixel's own term,
+// padded pixel (i+1, j+1), with its segment's mode): input rows 1 and n-2 and columns 1 and m-2
+// also read the padded border lines (P = 0 / n+1, Q = 0 / m+1; refl_sources), which the epilogue
+// left in fb.  Thread = (sample, border input pixel, 4 channels); the modes are linear in the
+// folded value, so the terms are added to what the epilogue stored (a masked pixel stays 0).
+// Needs n, m >= 4 (rows 1 and n-2 distinct).
+// --------------------------------------------------------------------------------------------
+struct FoldFixArgs {
+    const float *fb;        // (B, 2 (m+2) + 2 n, N)
+    int N, B, n, m;
+    FoldSeg seg[2];
+    int fsplit;
+};
+
+__global__ __launch_bounds__(256) void fold_fix_kernel(const FoldFixArgs a) {
+    const int g4 = a.N / 4, n = a.n, m = a.m;
+    const int nb = 2 * m + 2 * (n - 2);                     // border input pixels per sample
+    const long total = (long)a.B * nb * g4;
+    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const bool live = idx0 < total;
+    const bool pub = a.seg[0].amax || a.seg[1].amax;
+    if (!pub && !live) return;                               // (a block that publishes keeps every thread)
+    const long idx = live ? idx0 : total - 1;
+    const int c = (int)(idx % g4) * 4;
+    const long r = idx / g4;
+    const int k = (int)(r % nb), b = (int)(r / nb);
+    int i, j;
+    if (k < 2 * m) {                                         // rows 1 and n-2, every column
+        i = k < m ? 1 : n - 2;
+        j = k < m ? k : k - m;
+    } else {                                                 // columns 1 and m-2 of the other rows
+        const int k2 = k - 2 * m, rr = k2 >> 1;              // rows 0, 2 .. n-3, n-1
+        i = rr == 0 ? 0 : (rr <= n - 4 ? rr + 1 : n - 1);
+        j = (k2 & 1) ? m - 2 : 1;
+    }
+    int ys[3], xs[3];
+    const int ny = refl_sources(i, n, ys), nx = refl_sources(j, m, xs);
+    const int L = 2 * (m + 2) + 2 * n;
+    float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int u = 0; u < ny; ++u)
+        for (int v = 0; v < nx; ++v) {
+            if (u == 0 && v == 0) continue;                  // (i+1, j+1): the epilogue's own term
+            const float4 t = *(const float4 *)(a.fb + ((size_t)b * L + fold_border_index(ys[u], xs[v], n, m)) * a.N + c);
+            s.x += t.x; s.y += t.y; s.z += t.z; s.w += t.w;
+        }
+    const bool s1 = c >= a.fsplit;
+    const FoldSeg &S = s1 ? a.seg[1] : a.seg[0];
+    float mx = 0.0f;
+    if (live && S.dst) {
+        const size_t o = (((size_t)b * n + i) * m + j) * S.Cd + S.dc0 + c - (s1 ? a.fsplit : 0);
+        float4 f = make_float4(s.x * S.scale, s.y * S.scale, s.z * S.scale, s.w * S.scale);
+        if (S.mode == FOLD_MASK) {
+            const float4 mk = *(const float4 *)(S.aux + o);
+            f.x = mk.x > 0.f ? f.x : 0.f; f.y = mk.y > 0.f ? f.y : 0.f;
+            f.z = mk.z > 0.f ? f.z : 0.f; f.w = mk.w > 0.f ? f.w : 0.f;
+        }
+        float4 *d = (float4 *)(S.dst + o);
+        float4 v = *d;
+        v.x += f.x; v.y += f.y; v.z += f.z; v.w += f.w;
+        *d = v;
+        mx = amax4f(0.0f, v);
+        if (S.mode == FOLD_DST2 && S.aux) {
+            float4 *d2 = (float4 *)(S.aux + o);
+            float4 w = *d2;
+            w.x += f.x; w.y += f.y; w.z += f.z; w.w += f.w;
+            *d2 = w;
+        }
+    }
+    if (a.seg[0].amax) amax_publish(a.seg[0].amax, s1 ? 0.0f : mx);
+    if (a.seg[1].amax) amax_publish(a.seg[1].amax, s1 ? mx : 0.0f);
 }
 
 // dgrad weight packing: B fragment of the dgrad conv = W[k=cout][col=cin] at the flipped tap

@@ -135,11 +135,40 @@ enum Epi {
                          // (phase a*2+b, channel); a half-res pixel (i, j) yields u at the
                          // full-res pixel (2i+a, 2j+b) -- the q planes are full resolution
     EPI_UP4_Q_SAVE = 10, // ... and stores u (out1, full-res NHWC)
-    EPI_PH4 = 11         // out = acc: the stride-2 W0 dgrad as a four-phase conv over G (STAGE_ZP2):
+    EPI_PH4 = 11,        // out = acc: the stride-2 W0 dgrad as a four-phase conv over G (STAGE_ZP2):
                          // packed column = (phase a*2+b, channel); phase-grid pixel (i, j) is the
                          // padded-domain input-gradient pixel (2i+a, 2j+b) of a (2 Hout, 2 Wout)
                          // NHWC tensor; a wave skips the taps its phase has no weight on
+    EPI_FOLD = 12        // training dgrad (STAGE_ZP2) with the reflect fold in the epilogue: a
+                         // padded-domain output pixel (P, Q) inside [1, Hin] x [1, Win] IS the
+                         // input gradient at (P-1, Q-1) up to the reflected border sources, and is
+                         // written straight to its destination(s) (FoldSeg modes); the padded
+                         // border lines go to a compact buffer that fold_fix_kernel adds onto input
+                         // rows 1, Hin-2 and columns 1, Win-2 (reference ReflectionPad2d backward)
 };
+
+// EPI_FOLD destination of a range of packed output columns (the input-gradient channels of one
+// input tensor of the forward conv): dst (B, Hin, Win, Cd), channels dc0 + (column - first column
+// of the segment).  mode: FOLD_SET dst = s f; FOLD_ADD dst = aux + s f (aux = an addend laid out as
+// dst, or dst itself to accumulate); FOLD_MASK dst = (aux > 0) ? s f : 0 (aux = a ReLU mask laid out
+// as dst); FOLD_DST2 dst = s f and aux += s f (a second destination).  dst NULL: the columns are
+// discarded.  amax: publish max |dst| to these gradient-scale slots (NULL: none).
+enum FoldMode { FOLD_SET = 0, FOLD_ADD = 1, FOLD_MASK = 2, FOLD_DST2 = 3 };
+struct FoldSeg {
+    float *dst;
+    float *aux;
+    int Cd, dc0, mode;
+    float scale;
+    unsigned *amax;
+};
+
+// compact index of a border-line pixel of the (n+2) x (m+2) padded domain: row 0, row n+1, then
+// columns 0 and m+1 of rows 1..n -- 2 (m+2) + 2 n pixels per sample
+__host__ __device__ __forceinline__ int fold_border_index(int P, int Q, int n, int m) {
+    if (P == 0) return Q;
+    if (P == n + 1) return (m + 2) + Q;
+    return 2 * (m + 2) + 2 * (P - 1) + (Q == 0 ? 0 : 1);
+}
 
 struct ConvArgs {
     const float *in0;    // input segment 0, NHWC, c0 channels
@@ -176,6 +205,11 @@ struct ConvArgs {
     // m-tile partly idle), so the 16 lanes of an m-tile read 16 contiguous halo slots -- one
     // conflict-free ds_read_b128 lane group -- also when TW % 16 != 0
     int pitch;
+    // EPI_FOLD: packed columns [0, fsplit) -> fseg[0], [fsplit, N) -> fseg[1]; the padded border
+    // lines (B, 2 (Win+2) + 2 Hin, N) -> fborder (fold_border_index)
+    FoldSeg fseg[2];
+    int fsplit;
+    float *fborder;
 };
 
 // workgroup-local pixel index p -> tile coordinates; false for the idle lanes (beyond the
@@ -693,6 +727,147 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
     return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, ldexpf(1.0f, e0))));
 }
 
+// Gradient |x| maximum slots (the power-of-two gradient scales of the split-f16 dgrad / wgrad):
+// a workgroup maximum, then one atomicMax of its bits (non-negative floats order as unsigned;
+// fmaxf drops NaN, inf stays inf) into one of AMAX_SLOTS slots on separate 64-B lines.
+constexpr int AMAX_SLOTS = 256, AMAX_STRIDE = 16;
+__device__ __forceinline__ float amax4f(float m, const float4 &v) {
+    return fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
+}
+// the same reduction over NWV waves through caller-provided LDS scratch (red[NWV])
+template <int NWV>
+__device__ __forceinline__ void wg_amax_publish(float *red, unsigned *slots, float m) {
+    __syncthreads();                            // earlier reads of red are done
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float bm = red[0];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) bm = fmaxf(bm, red[w]);
+        if (bm > 0.0f) atomicMax(slots + (blockIdx.x & (AMAX_SLOTS - 1)) * AMAX_STRIDE, __float_as_uint(bm));
+    }
+}
+
+// EPI_FOLD epilogue (training dgrads, STAGE_ZP2): the accumulators hold the gradient of the
+// conv's reflect-padded input on the padded (Hin+2) x (Win+2) domain.  A padded pixel (P, Q) with
+// 1 <= P <= Hin, 1 <= Q <= Win is the input pixel (P-1, Q-1)'s own term of the reflect fold
+// (reference: autograd through ReflectionPad2d, base_layers.py ConvLayer) and goes straight to the
+// destination of its column's segment with that segment's mode (FoldSeg); the border-line pixels
+// (P or Q on the pad) go to the compact buffer fborder, from which fold_fix_kernel adds the
+// reflected terms onto input rows 1, Hin-2 and columns 1, Win-2.  Same per-wave LDS transpose,
+// aux-input ring and store order as the generic epilogue below (one aux input per segment).
+template <int MT_W, int NW, int WM, int NWV>
+__device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *smem, f32x4 (&acc)[MT_W][NW], int b,
+                                                   int oy0, int ox0, int wm, int nt0) {
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    constexpr int NTH = NWV * 64;
+    constexpr int LDT = NW * 16 + 4;
+    constexpr int CG = NW * 4;                              // 4-channel groups per pixel of the wave
+    constexpr int NIT = 16 * CG / 64;                       // items per lane per m-tile
+    constexpr int NPXB = MT_W * WM * 16;
+    static_assert(64 % CG == 0, "a lane's channel group must be the same for every item");
+    float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
+    int *ptab = reinterpret_cast<int *>(smem) + NWV * 16 * LDT;
+    const int n = a.Hin, mw = a.Win, L = 2 * (mw + 2) + 2 * n;
+    // ptab: input pixel index (interior), -(compact border index) - 2 (border line), -1 (outside)
+    for (int p = threadIdx.x; p < NPXB; p += NTH) {
+        int v = -1, py, px;
+        if (tile_pixel(a, p, py, px)) {
+            const int oy = oy0 + py, ox = ox0 + px;
+            if (oy < a.Hout && ox < a.Wout)
+                v = (oy >= 1 && oy <= n && ox >= 1 && ox <= mw) ? (b * n + oy - 1) * mw + ox - 1
+                                                                 : -(b * L + fold_border_index(oy, ox, n, mw)) - 2;
+        }
+        ptab[p] = v;
+    }
+    __syncthreads();
+    const int grp = lane >> 4, col = lane & 15;
+    const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
+    const int ch = (nt0 + q) * 16 + c4;                     // packed column = input-gradient channel
+    // the lane's segment is fixed (its channel group is the same for every item)
+    const bool s1 = ch >= a.fsplit;
+    float *const dst = s1 ? a.fseg[1].dst : a.fseg[0].dst;
+    float *const aux = s1 ? a.fseg[1].aux : a.fseg[0].aux;
+    const int Cd = s1 ? a.fseg[1].Cd : a.fseg[0].Cd;
+    const int mode = s1 ? a.fseg[1].mode : a.fseg[0].mode;
+    const float fs = s1 ? a.fseg[1].scale : a.fseg[0].scale;
+    const int chd = (s1 ? a.fseg[1].dc0 : a.fseg[0].dc0) + ch - (s1 ? a.fsplit : 0);
+    const bool has_aux = mode != FOLD_SET && aux != nullptr;
+    // branch-free aux reads (a branch makes the compiler drain vmcnt at the join): a lane without
+    // an aux input reads fborder[0..3] (valid memory) and ignores it
+    const float *abase = has_aux ? aux + chd : a.fborder;
+    const float4 bias4 = *(const float4 *)(a.bias + ch);
+    auto load_aux = [&](int m, float4 (&A)[NIT]) {
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
+            const unsigned o = has_aux ? (unsigned)(off < 0 ? 0 : off) * (unsigned)Cd : 0u;
+            A[it] = *(const float4 *)(abase + o);
+        }
+    };
+    constexpr int PD0 = CISTA_AUX_VGPRS / (NIT * 4);
+    constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
+    float4 ring[PD][NIT];
+#pragma unroll
+    for (int d = 0; d < PD; ++d) load_aux(d, ring[d]);
+    float mx = 0.0f;
+#pragma unroll
+    for (int m = 0; m < MT_W; ++m) {
+        float4 (&cur)[NIT] = ring[m % PD];
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int nn = 0; nn < NW; ++nn)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) T[(4 * grp + j) * LDT + nn * 16 + col] = acc[m][nn][j];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+        float4 rm[NIT], r2m[NIT];
+        int om[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int row = (it * 64 + lane) / CG;
+            const int off = ptab[(wm * MT_W + m) * 16 + row];
+            const float *src = T + row * LDT + q * 16 + c4;
+            const float v[4] = {src[0] + bias4.x, src[1] + bias4.y, src[2] + bias4.z, src[3] + bias4.w};
+            const float *A = reinterpret_cast<const float *>(&cur[it]);
+            float r[4], r2[4];
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+                const float f = v[e] * fs;
+                r[e] = mode == FOLD_ADD ? A[e] + f : (mode == FOLD_MASK ? (A[e] > 0.0f ? f : 0.0f) : f);
+                r2[e] = A[e] + f;
+                if (off < 0) r[e] = v[e];                  // border line: the raw padded-domain value
+            }
+            rm[it] = make_float4(r[0], r[1], r[2], r[3]);
+            r2m[it] = make_float4(r2[0], r2[1], r2[2], r2[3]);
+            om[it] = off;
+            if (off >= 0) mx = amax4f(mx, rm[it]);
+        }
+        // refill this ring slot before this m-tile's stores (vmcnt is in order)
+        if (m + PD < MT_W) load_aux(m + PD, cur);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int it = 0; it < NIT; ++it) {
+            const int off = om[it];
+            if (off >= 0) {
+                const unsigned o = (unsigned)off * (unsigned)Cd + (unsigned)chd;
+                if (dst) *(float4 *)(dst + o) = rm[it];
+                if (mode == FOLD_DST2 && aux) *(float4 *)(aux + o) = r2m[it];
+            } else if (off <= -2) {
+                *(float4 *)(a.fborder + (unsigned)(-off - 2) * (unsigned)a.N + (unsigned)ch) = rm[it];
+            }
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+    }
+    float *red = reinterpret_cast<float *>(smem) + a.lds_flag;
+    if (a.fseg[0].amax) wg_amax_publish<NWV>(red, a.fseg[0].amax, s1 ? 0.0f : mx);
+    if (a.fseg[1].amax) wg_amax_publish<NWV>(red, a.fseg[1].amax, s1 ? mx : 0.0f);
+}
+
 // ------------------------------------------------------------------------------------------
 // The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
 // MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
@@ -1046,6 +1221,11 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
         return;
     }
 
+    if constexpr (EPI == EPI_FOLD) {
+        conv_fold_epilogue<MT_W, NW, WM, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0);
+        return;
+    }
+
     // Epilogue through a per-wave LDS transpose: each m-tile's 16 pixels x (NW*16) columns are
     // written to LDS as [pixel][column] and read back so that a lane owns 4 consecutive
     // channels of one pixel -> the aux reads and output writes are 16-byte, fully coalesced
@@ -1113,7 +1293,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
     // m-tile's worth after each m-tile is consumed): under load an HBM read takes ~5 us, so a
     // one-ahead prefetch made the epilogue a chain of MT_W round trips (scripts/stamps.py)
     constexpr int AUXV = NIT * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
-    constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / AUXV : MT_W;   // 8 waves: 128-VGPR budget
+    constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / (AUXV ? AUXV : 1) : MT_W;   // 8 waves: 128-VGPR budget
     constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
     float4 ringA0[PD][NIT], ringA1[PD][NIT];
 #pragma unroll
