@@ -1,5 +1,5 @@
 """Per-layer kernel timing of one libcista_hip.so build (A/B of tiling variants).
-usage: CISTA_HIP_LIB=path python scripts/layer_bench.py [B]"""
+usage: CISTA_HIP_LIB=path python scripts/layer_bench.py [B [H W]]"""
 import json
 import os
 import sys
@@ -11,7 +11,7 @@ import bench  # noqa: E402
 from v2e2v_amd import CistaLSTCNet, _lib  # noqa: E402
 
 B = int(sys.argv[1]) if len(sys.argv) > 1 else 64
-H, W = 180, 240
+H, W = (int(sys.argv[2]), int(sys.argv[3])) if len(sys.argv) > 3 else (180, 240)
 dev = torch.device("cuda", 0)
 m = CistaLSTCNet([H, W])
 bench.he_init_(torch, m, 7)

@@ -300,6 +300,28 @@ def test_batch_equals_single_two_frames():
             assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
 
 
+def test_batch48_persistent_equals_single():
+    """At B=48, 180x240 every 128-column conv has 2880 (pixel tile, column block) items, several
+    per resident workgroup: a persistent build (CISTA_PERSIST, each workgroup walking items with
+    the next item's first halo chunk fetched by LDS-DMA during the epilogue) must give every
+    sample exactly its B=1 result, whose launches fit the chip and run one item per workgroup."""
+    params = fx.stress_params(64, 5, 5, seed=33)
+    m = make_model(params=params)
+    B = 48
+    rng = np.random.default_rng(9)
+    vox = gpu(rng.standard_normal((2, B, 5, 180, 240)).astype(np.float32))
+    prev = torch.rand(B, 1, 180, 240, device=DEV)
+    with torch.no_grad():
+        r, s = m(vox[0], prev, None)
+        r, s = m(vox[1], r, s)
+        for i in (0, 17, 47):
+            ri, si = m(vox[0, i:i + 1], prev[i:i + 1], None)
+            ri, si = m(vox[1, i:i + 1], ri, si)
+            assert torch.equal(r[i:i + 1], ri), i
+            assert torch.equal(s[0][i:i + 1], si[0]) and torch.equal(s[1][i:i + 1], si[1]), i
+            assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
+
+
 def test_determinism_and_batch_independence():
     """Size-independent properties at the bench size: bit-identical re-runs, and sample i of a
     batched launch equals the same sample run alone (no cross-sample coupling)."""

@@ -208,7 +208,23 @@ bool allow_big_lds(const void *kern) {
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2>
+// compute units of the current device (persistent launches size their grid by it)
+[[maybe_unused]] int device_cus() {
+    static std::mutex mu;
+    static int cus[64] = {0};
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!cus[dev]) {
+        int n = 0;
+        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
+        cus[dev] = n;
+    }
+    return cus[dev];
+}
+
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2,
+          bool PERS = false>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
@@ -230,13 +246,14 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
     // the training variant (SV) only for epilogues that save activations, and only when asked
     constexpr bool HAS_SV = EPI == EPI_ISTA_P || EPI == EPI_LSTC_CELL || EPI == EPI_LSTC_OUT || EPI == EPI_LSTM;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false, OCC>;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false, OCC, PERS>;
     if constexpr (HAS_SV)
         if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr)
-            kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC>;
+            kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC, PERS>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
 #if CISTA_XCD
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
+    static_assert(!PERS || CISTA_XCD, "persistent items use the 1-D grid");
 #else
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
 #endif
@@ -251,6 +268,17 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
     const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
+    if constexpr (PERS) {
+        // one workgroup per resident slot walking the items (dma_chunk0); only where every slot
+        // gets more than one item, the epilogue's LDS fits in the first staging image (the raw
+        // image of the next item lands in the second) and the tile is not a border strip
+        const long items = (long)a.B * t.ty * t.tx * (a.N / nblk_cols);
+        const long slots = (long)device_cus() * (OCC * 4 / NWV);
+        if (items <= slots || t.lds / 2 < epi_lds + 12 * NWV || a.border != 0 || (slots & 7))
+            return launch_conv_cfg<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, OCC, false>(a, st);
+        a.items = (int)items;
+        grid = dim3((unsigned)slots);
+    }
     hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
@@ -283,6 +311,9 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #endif
 #ifndef CISTA_DGRAD_SMALL
 #define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
+#endif
+#ifndef CISTA_PERSIST
+#define CISTA_PERSIST 0   // forward stride-1 convs at large batch: persistent items, next tile's chunk 0 by LDS-DMA
 #endif
 #ifndef CISTA_WIDE
 #define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
@@ -344,13 +375,14 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
             if (a.N == 128 && CISTA_ISTA8 > 1) return launch_conv_cfg<6, 2, 2, 4, STAGE, EPI, G, true, 2, 4>(a, st);
             if (a.N == 64) return launch_conv_cfg<3, 2, 4, 2, STAGE, EPI, G, true, 2, 4>(a, st);
         }
+        constexpr bool PS = STAGE == STAGE_S1 && CISTA_PERSIST;   // (falls back per launch, launch_conv_cfg)
         if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
-            if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4, 2, PS>(a, st);
         if constexpr (G == 4) {
             if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
         } else {
-            if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4>(a, st);
-            if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4, 2, PS>(a, st);
+            if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4, 2, PS>(a, st);
             if (a.N == 32) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);
         }
         return CISTA_ERR_UNSUPPORTED;

@@ -210,6 +210,7 @@ struct ConvArgs {
     FoldSeg fseg[2];
     int fsplit;
     float *fborder;
+    int items;           // persistent launches: (pixel tile, column block) items of the grid
 };
 
 // workgroup-local pixel index p -> tile coordinates; false for the idle lanes (beyond the
@@ -440,12 +441,12 @@ __device__ float stage_absmax(const ConvArgs &a, int b, int iy0, int ix0, int HH
 // spix: pixel index (b, iy, ix) >= 0, -1 = no item, -2 = zero padding (STAGE_ZP2).
 template <int STAGE, int NI, int NT = 256>
 __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd,
-                                             int (&spix)[NI], int (&hps)[NI], int (&gs)[NI]) {
+                                             int (&spix)[NI], int (&hps)[NI], int (&gs)[NI], int tid) {
     const int HP = HH * HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
-        const int it = threadIdx.x + u * NT;
+        const int it = tid + u * NT;
         const int hp = ((it >> 5) << 3) | (it & 7);
         gs[u] = (it >> 3) & 3;
         hps[u] = (it < nitems && hp < HP) ? hp : -1;
@@ -594,8 +595,8 @@ __device__ __forceinline__ void rare_item(const ConvArgs &a, int b, int iy0, int
 
 template <int MT_W, int WM, int NW, int STAGE, int NWV = 4>
 __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32x4 (&acc)[MT_W][NW], int b, int oy0,
-                                             int ox0, int wm, int nt0, int nchunks, int kc0) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+                                             int ox0, int wm, int nt0, int nchunks, int kc0, int tid) {
+    const int lane = tid & 63, wave = tid >> 6;
     constexpr int S = (STAGE == STAGE_S2) ? 2 : 1;
     const int HWd = (a.TW - 1) * S + 3, HH = (a.TH - 1) * S + 3;
     const int HP = HH * HWd;
@@ -613,7 +614,7 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
     for (int kc = 0; kc < nchunks; ++kc) {
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
-        for (int it = threadIdx.x; it < nitems; it += NWV * 64) {
+        for (int it = tid; it < nitems; it += NWV * 64) {
             const int hp = ((it >> 5) << 3) | (it & 7);
             if (hp >= HP) continue;
             float4 v0, v1;
@@ -678,7 +679,7 @@ __device__ __forceinline__ float range_rerun(const ConvArgs &a, u32x4 *smem, f32
         const float *seg; int segC, choff;
         seg_of(kc, seg, segC, choff);
         __syncthreads();                                // the maxima / previous chunk's reads are done
-        for (int it = threadIdx.x; it < nitems; it += NWV * 64) {
+        for (int it = tid; it < nitems; it += NWV * 64) {
             const int hp = ((it >> 5) << 3) | (it & 7), g = (it >> 3) & 3;
             if (hp >= HP) continue;
             float4 v0, v1;
@@ -875,51 +876,78 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
 // SV: training variant -- the epilogue also stores the activations the BPTT backward needs
 // (out1 / out2, see ConvArgs); the inference variant has no such stores in its epilogue.
 // OCC: workgroups per CU the register budget is sized for (LDS: the host's tile choice)
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false,
-          int OCC = 2>
-__global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvArgs a) {
-    // NI > 0: double-buffered K loop (two LDS images, next chunk's loads in NI x 8 VGPRs)
-    constexpr int NWV = WM * WN, NTH = NWV * 64;           // waves, threads
-    static_assert(NWV == 4 || NWV == 8, "4 or 8 waves per workgroup");
-    static_assert(NW % G == 0, "a wave must hold whole gate groups");
-    extern __shared__ u32x4 smem[];
-
+// Persistent mode (PERS): the grid is one workgroup per resident slot and each workgroup walks a
+// range of (pixel tile, column block) items.  The NEXT item's first K-chunk halo is fetched with
+// LDS-DMA (global_load_lds_dwordx4: no VGPRs, so nothing is held across the epilogue) into the
+// second staging image's area while this item's epilogue runs, and split into hi / lo at the
+// next item's start: the per-tile prologue HBM round trip (~9 k cycles of a ~75 k-cycle tile,
+// DESIGN.md 4.7) overlaps the epilogue instead of stalling the next workgroup.  Raw image: piece
+// P = hp * 8 + q (16 B: channels 4q .. 4q+3 of halo pixel hp), lane-linear per wave instruction.
+template <int STAGE, int NWV>
+__device__ __forceinline__ void dma_chunk0(const ConvArgs &a, u32x4 *raw, int tile) {
+    static_assert(STAGE == STAGE_S1, "persistent staging: reflect-padded stride-1 convs");
     const int lane = threadIdx.x & 63;
-    const int wave = threadIdx.x >> 6;
-#if CISTA_STAMPS
-    {
-        unsigned hw, xcc;
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
-        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
-        CISTA_STAMP(0, (unsigned long long)hw | ((unsigned long long)xcc << 32));
-        CISTA_STAMP(13, __builtin_amdgcn_s_memrealtime());
-        CISTA_STAMP(1, __builtin_amdgcn_s_memtime());
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    int t = tile;
+    const int tx = t % a.tiles_x;
+    t /= a.tiles_x;
+    const int ty = t % a.tiles_y;
+    const int b = t / a.tiles_y;
+    const int iy0 = ty * a.TH - 1, ix0 = tx * a.TW - 1;
+    const int HWd = a.TW + 2, HP = (a.TH + 2) * HWd, npieces = HP * 8;
+    for (int u = 0; u * NWV * 64 < npieces; ++u) {
+        const int base = (u * NWV + wave) * 64;
+        const int P = base + lane;
+        if (P < npieces) {
+            const int hp = P >> 3, q = P & 7;
+            const int hy = hp / HWd, hx = hp - hy * HWd;
+            const int iy = reflect_clamp(iy0 + hy, a.Hin), ix = reflect_clamp(ix0 + hx, a.Win);
+            const float *g = a.in0 + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.c0 + 4 * q;
+            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
+                                             (__attribute__((address_space(3))) void *)(raw + base), 16, 0, 0);
+        }
     }
-#endif
-#if CISTA_EXP_JITTER
-    if (blockIdx.x < 512u) {
-        const unsigned hsh = (blockIdx.x * 2654435761u) >> 16;
-        const unsigned long long until = __builtin_amdgcn_s_memtime() + (unsigned long long)(hsh % 1024u) * CISTA_EXP_JITTER / 1024u;
-        while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(4);
+}
+
+// raw chunk-0 image (dma_chunk0) -> hi / lo staging image 0, the items of stage_commit
+template <int NI>
+__device__ __forceinline__ void raw_commit(u32x4 *buf, const u32x4 *raw, int HPpad, const int (&hps)[NI],
+                                           const int (&gs)[NI], f16x2 &amax) {
+#pragma unroll
+    for (int u = 0; u < NI; ++u) {
+        if (hps[u] < 0) continue;
+        const float4 v0 = __builtin_bit_cast(float4, raw[hps[u] * 8 + 2 * gs[u]]);
+        const float4 v1 = __builtin_bit_cast(float4, raw[hps[u] * 8 + 2 * gs[u] + 1]);
+        u32x4 hi, lo;
+        split8(v0, v1, hi, lo, amax);
+        buf[gs[u] * HPpad + hps[u]] = hi;
+        buf[(4 + gs[u]) * HPpad + hps[u]] = lo;
     }
-#endif
+}
+
+// one (pixel tile, column block) item of the conv (the body of conv3x3_split3, below)
+// from_raw: the item's chunk-0 halo is already in the raw image (PERS); next_item >= 0: DMA the
+// next item's chunk 0 during this item's epilogue (PERS)
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI, bool SV, bool PERS>
+__device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsigned witem, bool from_raw,
+                                          int next_item) {
+    constexpr int NWV = WM * WN, NTH = NWV * 64;           // waves, threads
+    int tid = threadIdx.x;
+    // PERS: an opaque thread id per item, so that nothing thread-derived (halo items, A / B
+    // addresses, the epilogue's channel constants) is hoisted out of the item loop and held
+    // across it (the hoisted values spilled 50-65 VGPRs in the 250-VGPR convs)
+    if constexpr (PERS) asm volatile("" : "+v"(tid));
+    const int lane = tid & 63;
+    const int wave = tid >> 6;
     const int wm = wave % WM;
     const int wn = wave / WM;
 #if CISTA_XCD
-    // XCD-aware work order: workgroup L runs on XCD L % 8 (round-robin dispatch), so every XCD
-    // is given a contiguous range of (pixel tile, column block) items, the column blocks of a
-    // tile back to back: the halo a tile shares with its column-block siblings and with its
-    // neighbouring tiles is re-read from that XCD's L2 (bijective for any grid size)
-    const unsigned witem = [] {
-        const unsigned total = gridDim.x, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
-        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
-    }();
     const unsigned nnb = (unsigned)a.N / (unsigned)(WN * NW * 16);
     const int nblk = (int)(witem % nnb);
     int t = (int)(witem / nnb);
 #else
     const int nblk = blockIdx.y;
-    int t = blockIdx.x;
+    int t = (int)witem;
 #endif
     const int tx = t % a.tiles_x;
     t /= a.tiles_x;
@@ -1001,8 +1029,15 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
                           STAGE == STAGE_S2D,
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
-        stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg);
-        {
+        stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg, tid);
+        if (PERS && from_raw) {
+            // chunk 0 arrived by LDS-DMA during the previous item's epilogue (raw image in the
+            // second staging image's area): every wave's DMAs have landed, and every wave is done
+            // with the epilogue's LDS (the first image's area), before the split writes image 0
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+            raw_commit<NI>(smem, smem + 8 * HPpad, HPpad, shp, sg, amax);
+        } else {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
             float4 sv0[NI], sv1[NI];
@@ -1130,7 +1165,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
 #pragma unroll
         for (int w = 1; w < NWV; ++w) anyfl |= fl[w];
         if (CISTA_RERUN && !a.ascale && anyfl != 0)
-            insc = range_rerun<MT_W, WM, NW, STAGE, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0);
+            insc = range_rerun<MT_W, WM, NW, STAGE, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0, tid);
     }
 
     // ---------------------------------- epilogue ----------------------------------------
@@ -1169,7 +1204,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
         // waiting behind the stores before it (vmcnt is in order)
         __syncthreads();                                   // the last chunk's A reads are done
         float *wfs = reinterpret_cast<float *>(smem);
-        for (int i = threadIdx.x; i < 9 * a.Cout; i += NTH) wfs[i] = a.aux0[i];
+        for (int i = tid; i < 9 * a.Cout; i += NTH) wfs[i] = a.aux0[i];
         __syncthreads();
 #pragma unroll
         for (int m = 0; m < MT_W; ++m) {
@@ -1239,7 +1274,7 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
     // per-pixel element offset (pixel * Cout) of the output tensors, -1 outside the image:
     // the items below then need no division, no 64-bit math and no bounds arithmetic
     int *ptab = reinterpret_cast<int *>(smem) + NWV * 16 * LDT;
-    for (int p = threadIdx.x; p < NPXB; p += NTH) {
+    for (int p = tid; p < NPXB; p += NTH) {
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
@@ -1251,6 +1286,11 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
     }
     __syncthreads();
     CISTA_STAMP(15, __builtin_amdgcn_s_memtime());
+    // PERS: the next item's chunk 0 into the raw image (the second staging image's area; this
+    // epilogue's LDS is in the first).  Issued after the epilogue's last workgroup barrier: a
+    // barrier would drain it (hipcc waits vmcnt(0) at __syncthreads while an LDS-DMA is in flight)
+    if constexpr (PERS)
+        if (next_item >= 0) dma_chunk0<STAGE, NWV>(a, smem + 8 * HPpad, next_item / (int)((unsigned)a.N / (unsigned)(WN * NW * 16)));
     const int grp = lane >> 4;
     // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
     const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
@@ -1456,6 +1496,65 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
         }
     CISTA_STAMP(12, __builtin_amdgcn_s_memtime());
     CISTA_STAMP(14, __builtin_amdgcn_s_memrealtime());
+}
+
+// ------------------------------------------------------------------------------------------
+// The conv kernel.  Workgroup = WM x WN waves; one (pixel tile, column block) item per
+// workgroup, or (PERS) a range of items per workgroup (dma_chunk0 above).
+// ------------------------------------------------------------------------------------------
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false,
+          int OCC = 2, bool PERS = false>
+__global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvArgs a) {
+    constexpr int NWV = WM * WN;
+    static_assert(NWV == 4 || NWV == 8, "4 or 8 waves per workgroup");
+    static_assert(NW % G == 0, "a wave must hold whole gate groups");
+    static_assert(!PERS || (STAGE == STAGE_S1 && NI > 0 && EPI != EPI_FOLD && EPI != EPI_PH4 && EPI != EPI_UP_Q &&
+                            EPI != EPI_UP_Q_SAVE && EPI != EPI_UP4_Q && EPI != EPI_UP4_Q_SAVE),
+                  "persistent items: double-buffered stride-1 convs with the generic epilogue");
+    extern __shared__ u32x4 smem[];
+#if CISTA_STAMPS
+    {
+        unsigned hw, xcc;
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(hw));
+        asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+        CISTA_STAMP(0, (unsigned long long)hw | ((unsigned long long)xcc << 32));
+        CISTA_STAMP(13, __builtin_amdgcn_s_memrealtime());
+        CISTA_STAMP(1, __builtin_amdgcn_s_memtime());
+    }
+#endif
+#if CISTA_EXP_JITTER
+    if (blockIdx.x < 512u) {
+        const unsigned hsh = (blockIdx.x * 2654435761u) >> 16;
+        const unsigned long long until = __builtin_amdgcn_s_memtime() + (unsigned long long)(hsh % 1024u) * CISTA_EXP_JITTER / 1024u;
+        while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(4);
+    }
+#endif
+    if constexpr (PERS) {
+        // XCD-aware: workgroup L runs on XCD L % 8 (round-robin dispatch; the grid is a multiple
+        // of 8); XCD x owns a contiguous range of the a.items items, walked by its workgroups in
+        // lock-step strides, so neighbouring tiles run together on one L2
+        const unsigned total = (unsigned)a.items, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
+        const unsigned x0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+        const unsigned x1 = x0 + q + (xcd < r ? 1u : 0u), step = gridDim.x >> 3;
+        bool first = true;
+        for (unsigned w = x0 + (L >> 3); w < x1; w += step, first = false)
+            conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV, PERS>(a, smem, w, !first,
+                                                                          w + step < x1 ? (int)(w + step) : -1);
+    } else {
+#if CISTA_XCD
+        // XCD-aware work order: workgroup L runs on XCD L % 8 (round-robin dispatch), so every XCD
+        // is given a contiguous range of (pixel tile, column block) items, the column blocks of a
+        // tile back to back: the halo a tile shares with its column-block siblings and with its
+        // neighbouring tiles is re-read from that XCD's L2 (bijective for any grid size)
+        const unsigned witem = [] {
+            const unsigned total = gridDim.x, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
+            return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+        }();
+#else
+        const unsigned witem = blockIdx.x;
+#endif
+        conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV, PERS>(a, smem, witem, false, -1);
+    }
 }
 
 // ------------------------------------------------------------------------------------------
