@@ -1,5 +1,6 @@
 """Which frame stage gives different bits for one sample run alone (B=1) and inside a batch?
-Each stage entry (include/cista_lstc.h) gets the same random inputs at B=12 and at B=1."""
+Each stage entry (include/cista_lstc.h) gets the same random inputs at B=Bb and at B=1.
+usage: python scripts/diag_batch_bits.py [Bb]"""
 import ctypes
 import sys
 import os
@@ -20,7 +21,7 @@ packed = m.packed_params()
 cfg = _lib.CistaConfig(64, 5, 5)
 L = _lib.lib()
 g = torch.Generator(device=dev).manual_seed(1)
-Bb = 12
+Bb = int(sys.argv[1]) if len(sys.argv) > 1 else 12
 R = lambda *s: torch.randn(*s, device=dev, generator=g)  # noqa: E731
 ev, img = R(Bb, 5, H, W), torch.rand(Bb, 1, H, W, device=dev, generator=g)
 x1, zp, cp = R(Bb, h, w, C), R(Bb, h, w, 2 * C), R(Bb, h, w, 2 * C)
