@@ -667,12 +667,11 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                     ConvArgs bo = conv_args_f(f, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
                     bo.out0 = f.full; bo.aux0 = blob<float>(f.packed, f.L.wF); bo.out1 = f.u;
                     bo.border = mode;
-                    // 64-pixel strip tiles at small batch (twice the workgroups: the B = 1 frame is
-                    // latency-bound), 128-pixel ones otherwise
-                    const int sb = B < 32 ? (f.u ? launch_conv_cfg<1, 4, 4, 1, STAGE_UP, EPI_UP_Q_SAVE, 1>(bo, f.st)
-                                                 : launch_conv_cfg<1, 4, 4, 1, STAGE_UP, EPI_UP_Q, 1>(bo, f.st))
-                                          : (f.u ? launch_conv_cfg<2, 4, 4, 1, STAGE_UP, EPI_UP_Q_SAVE, 1>(bo, f.st)
-                                                 : launch_conv_cfg<2, 4, 4, 1, STAGE_UP, EPI_UP_Q, 1>(bo, f.st));
+                    // 64-pixel strip tiles at every batch size: the 128-pixel configuration gave
+                    // border pixels that differ in the last bit from the 64-pixel one (batch
+                    // independence, tests/test_gpu_parity.py::test_batch48_persistent_equals_single)
+                    const int sb = f.u ? launch_conv_cfg<1, 4, 4, 1, STAGE_UP, EPI_UP_Q_SAVE, 1>(bo, f.st)
+                                       : launch_conv_cfg<1, 4, 4, 1, STAGE_UP, EPI_UP_Q, 1>(bo, f.st);
                     if (sb) return sb;
                 }
                 return CISTA_OK;

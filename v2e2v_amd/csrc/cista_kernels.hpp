@@ -64,6 +64,13 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_EXP_JITTER
 #define CISTA_EXP_JITTER 0
 #endif
+// MFMA issue order within an m-tile: 0 = per n-tile the three split products (hh, hl, lh);
+// 1 = per split product all n-tiles (the A operand changes 2 times in 3 NW MFMAs instead of
+// 2 NW times: fewer operand transitions under a clock held by power, MI355X_MICROARCH.md 'DVFS
+// give-back'); every accumulator still sums hh, hl, lh in that order (bit-identical)
+#ifndef CISTA_MFMA_ORDER
+#define CISTA_MFMA_ORDER 0
+#endif
 #ifndef CISTA_AORDER
 #define CISTA_AORDER 0
 #endif
@@ -539,6 +546,17 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
         }
         const f16x8 xh = __builtin_bit_cast(f16x8, ah[m & 1]);
         const f16x8 xl = __builtin_bit_cast(f16x8, al[m & 1]);
+        if constexpr (CISTA_MFMA_ORDER == 1) {
+#pragma unroll
+            for (int n = 0; n < NW; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, __builtin_bit_cast(f16x8, bh[n]), acc[m][n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NW; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, __builtin_bit_cast(f16x8, bl[n]), acc[m][n], 0, 0, 0);
+#pragma unroll
+            for (int n = 0; n < NW; ++n)
+                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, __builtin_bit_cast(f16x8, bh[n]), acc[m][n], 0, 0, 0);
+        } else {
 #pragma unroll
         for (int n = 0; n < NW; ++n) {
             const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
@@ -546,6 +564,7 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wh, acc[m][n], 0, 0, 0);
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wl, acc[m][n], 0, 0, 0);
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wh, acc[m][n], 0, 0, 0);
+        }
         }
 #if CISTA_AORDER
         // the next m-tile's two A reads go out BEFORE this m-tile's MFMAs (left to itself the
