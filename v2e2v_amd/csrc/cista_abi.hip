@@ -267,7 +267,11 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
+    size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
+#ifdef CISTA_EXP_ONEWG
+    // timing experiment: one workgroup per CU (LDS-limited), no overlap between workgroups
+    if (lds < 96 * 1024) lds = 96 * 1024;
+#endif
     if constexpr (PERS) {
         // one workgroup per resident slot walking the items (dma_chunk0); only where every slot
         // gets more than one item, the epilogue's LDS fits in the first staging image (the raw
@@ -510,6 +514,10 @@ int run_layer(const Frame &f, int layer, int it = 0) {
     const bool zstack = f.zl && f.cfg->depth > 0;
     float *z_in = zstack ? f.zl + (size_t)it * hw * 2 * f.C : f.z;
     float *z_out = zstack && it + 1 < f.cfg->depth ? f.zl + (size_t)(it + 1) * hw * 2 * f.C : f.z;
+#ifdef CISTA_EXP_ZOUT
+    // timing experiment (results wrong): ISTA P writes z to scratch instead of in place
+    if (!zstack && f.full) z_out = f.full;
+#endif
     const int C = f.C, B = f.B, h = f.h, w = f.w;
     ConvArgs a;
     switch (layer) {
