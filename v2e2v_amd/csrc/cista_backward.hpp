@@ -780,13 +780,6 @@ __device__ __forceinline__ void split4(const float4 &v, uint2 &hi, uint2 &lo) {
                     __builtin_bit_cast(unsigned, __builtin_convertvector(r23, h2)));
 }
 
-// register sets of the staging waves: 1 = the next tile's loads in flight during one tile
-// period, 2 = two tiles in flight (two periods to hide an HBM round trip under load)
-#ifndef CISTA_WT_DEPTH
-#define CISTA_WT_DEPTH 1
-#endif
-static_assert(CISTA_WT_DEPTH == 1 || CISTA_WT_DEPTH == 2, "wgrad_tr staging depth");
-
 __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
     _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
@@ -805,8 +798,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
     const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
-    // staging registers: set 0 (and, with CISTA_WT_DEPTH 2, set 1: two tiles in flight)
-    float4 gvs[CISTA_WT_DEPTH][6], xvs[CISTA_WT_DEPTH][9];
+    float4 gv[6], xv[9];
     auto tile_origin = [&](int tile, int &b, int &oy0, int &ox0) __attribute__((always_inline)) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
@@ -821,7 +813,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         const int hy = hp / WT_HW, hx = hp - hy * WT_HW;
         return wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
     };
-    auto load_tile = [&](int tile, float4 (&gv)[6], float4 (&xv)[9]) __attribute__((always_inline)) {
+    auto load_tile = [&](int tile) __attribute__((always_inline)) {
         int b, oy0, ox0;
         tile_origin(tile, b, oy0, ox0);
 #pragma unroll
@@ -845,7 +837,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + hp * 16 + 4 * sq) = lo;
     };
     // registers -> LDS buffer (hi / lo planes); publishes whether this wave's X overflowed
-    auto commit = [&](_Float16 *buf, int *flag, const float4 (&gv)[6], const float4 (&xv)[9]) __attribute__((always_inline)) {
+    auto commit = [&](_Float16 *buf, int *flag) __attribute__((always_inline)) {
         _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
 #pragma unroll
         for (int u = 0; u < 6; ++u) {
@@ -895,23 +887,15 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     if (loader) {
         // the roles run separate loops with the same barrier sequence, so the loaders' staging
         // registers and the MFMA waves' accumulators are never live at the same time
-        // tile k of this workgroup (k = 0, 1, ...: tile blockIdx.y + k nsplit) is staged from
-        // register set (k - 1) % DEPTH; DEPTH 2 issues tile k + 2's loads while committing tile
-        // k + 1, so each load has two tile periods (not one) to return from HBM
-        constexpr int DEPTH = CISTA_WT_DEPTH;
         if ((int)blockIdx.y < ntiles) {
-            load_tile(blockIdx.y, gvs[0], xvs[0]);
-            commit(sm, xfl, gvs[0], xvs[0]);
-#pragma unroll
-            for (int d = 0; d < DEPTH; ++d)
-                if ((int)blockIdx.y + (d + 1) * a.nsplit < ntiles) load_tile(blockIdx.y + (d + 1) * a.nsplit, gvs[d], xvs[d]);
+            load_tile(blockIdx.y);
+            commit(sm, xfl);
+            if ((int)blockIdx.y + a.nsplit < ntiles) load_tile(blockIdx.y + a.nsplit);
         }
         __syncthreads();
         int it = 0;
-#pragma unroll DEPTH
         for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
             const int bi = it & 1;
-            const int rs = it % DEPTH;             // register set of tile k + 1 = it + 1
             if (__builtin_expect(flagged(bi), 0)) {
                 __syncthreads();
                 int b, oy0, ox0;
@@ -932,14 +916,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
             }
             if (tile + a.nsplit < ntiles) {
                 // the other buffer was last read before the barrier that opened this iteration
-                if (DEPTH == 1 || rs == 0) {
-                    commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1), gvs[0], xvs[0]);
-                    if (tile + (DEPTH + 1) * a.nsplit < ntiles) load_tile(tile + (DEPTH + 1) * a.nsplit, gvs[0], xvs[0]);
-                } else {
-                    commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1), gvs[DEPTH - 1], xvs[DEPTH - 1]);
-                    if (tile + (DEPTH + 1) * a.nsplit < ntiles)
-                        load_tile(tile + (DEPTH + 1) * a.nsplit, gvs[DEPTH - 1], xvs[DEPTH - 1]);
-                }
+                commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1));
+                if (tile + 2 * a.nsplit < ntiles) load_tile(tile + 2 * a.nsplit);
             }
             __syncthreads();
         }

@@ -71,10 +71,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_MFMA_ORDER
 #define CISTA_MFMA_ORDER 0
 #endif
-// issue chunk 1's halo and chunk 0's first B taps in the prologue (see the double-buffered K loop)
-#ifndef CISTA_HOIST1
-#define CISTA_HOIST1 0
-#endif
 #ifndef CISTA_AORDER
 #define CISTA_AORDER 0
 #endif
@@ -1053,35 +1049,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
         stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg, tid);
-        // B fragments D taps ahead in a ring of D + 1 slots.  vmcnt is in order, so the wait
-        // for any B load issued after the next chunk's halo loads also waits for the halo (an
-        // HBM round trip, ~5 us under load): with D taps loaded before them, the first such wait
-        // is at tap D + 1.  HOIST (CISTA_HOIST1): chunk 0's first D taps of B and chunk 1's halo
-        // are issued in the prologue, before chunk 0's halo is waited for, so chunk 1's halo has
-        // the prologue's round trip to land and chunk 0's taps never wait behind it
-        constexpr int D = BPF;
-        constexpr bool HOIST = CISTA_HOIST1 != 0 && NW <= 2 && EPI != EPI_FOLD && !CISTA_EXP_NOSTAGE && !CISTA_EXP_NOB;
-        u32x4 bh[D + 1][NW], bl[D + 1][NW];
-        float4 sv0[NI], sv1[NI];                            // the next chunk's halo in flight
-        auto b_first = [&](const u32x4 *wp) __attribute__((always_inline)) {
-#pragma unroll
-            for (int t = 0; t < D; ++t)
-#pragma unroll
-                for (int n = 0; n < NW; ++n) {
-                    bh[t][n] = wp[(size_t)t * tapstride + n * 128];
-                    bl[t][n] = wp[(size_t)t * tapstride + n * 128 + 64];
-                }
-        };
-        auto hoisted = [&]() __attribute__((always_inline)) {
-            if constexpr (HOIST) {
-                b_first(a.wpack + (size_t)nt0 * 128 + lane);
-                if (nchunks > 1) {
-                    const float *seg; int segC, choff;
-                    seg_of(1, seg, segC, choff);
-                    stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1, b);
-                }
-            }
-        };
         if (PERS && from_raw) {
             // chunk 0 arrived by LDS-DMA during the previous item's epilogue (raw image in the
             // second staging image's area): every wave's DMAs have landed, and every wave is done
@@ -1089,14 +1056,12 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
             raw_commit<NI>(smem, smem + 8 * HPpad, HPpad, shp, sg, amax);
-            hoisted();
         } else {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
-            float4 c0v0[NI], c0v1[NI];
-            stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, c0v0, c0v1, b);
-            hoisted();
-            stage_commit<NI>(smem, HPpad, c0v0, c0v1, shp, sg, amax);
+            float4 sv0[NI], sv1[NI];
+            stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1, b);
+            stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
         }
         __syncthreads();
         CISTA_STAMP(2, __builtin_amdgcn_s_memtime());
@@ -1104,13 +1069,25 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
             const u32x4 *cur = smem + (kc & 1) * 8 * HPpad;
             u32x4 *nxt = smem + ((kc + 1) & 1) * 8 * HPpad;
             const bool more = kc + 1 < nchunks;
-            const bool first_hoisted = HOIST && kc == 0;    // chunk 0: B taps < D and chunk 1 in flight
             const float *nseg; int nsegC, nchoff;
             seg_of(more ? kc + 1 : kc, nseg, nsegC, nchoff);
 #pragma unroll
             for (int m = 0; m < MT_W; ++m) asm volatile("" : "+v"(abase[m]));
             const u32x4 *wp = a.wpack + ((size_t)kc * 9) * tapstride + (size_t)nt0 * 128 + lane;
-            if (!first_hoisted) b_first(wp);
+            // B fragments D taps ahead in a ring of D + 1 slots.  vmcnt is in order, so the wait
+            // for any B load issued after the next chunk's halo loads (tap 0) also waits for the
+            // halo (an HBM round trip, ~5 us under load): with D taps loaded before them, the
+            // first such wait is at tap D + 1
+            constexpr int D = BPF;
+            u32x4 bh[D + 1][NW], bl[D + 1][NW];
+#pragma unroll
+            for (int t = 0; t < D; ++t)
+#pragma unroll
+                for (int n = 0; n < NW; ++n) {
+                    bh[t][n] = wp[(size_t)t * tapstride + n * 128];
+                    bl[t][n] = wp[(size_t)t * tapstride + n * 128 + 64];
+                }
+            float4 sv0[NI], sv1[NI];
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 if (tap + D <= 8 && !CISTA_EXP_NOB) {
@@ -1121,7 +1098,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                         bl[(tap + D) % (D + 1)][n] = wq[n * 128 + 64];
                     }
                 }
-                if (tap == 0 && more && !CISTA_EXP_NOSTAGE && !first_hoisted)
+                if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
                     stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
 #if CISTA_PRIO == 1
                 __builtin_amdgcn_s_setprio(1);
