@@ -595,6 +595,20 @@ def dominant_roofline(layers, lib_mod, traffic_tag=None):
                 gbps = tl["hbm_bytes_per_launch"] / (dom["ms"] * 1e-3) / 1e9
                 roofline["hbm_achieved_GBps"] = round(gbps, 1)
                 roofline["hbm_frac"] = round(gbps / (HBM_TBPS * 1e3), 4)
+                # the same PMC run's SQ / GRBM counters of that kernel (rNN_pmc_counters.json,
+                # scripts/pmc_summary.py): the clock the chip held over the launch (GRBM_GUI_ACTIVE
+                # / 8 XCDs / duration) and the matrix pipes' busy share of those cycles; the peak
+                # above assumes 2.4 GHz, the convs run power-limited below it
+                cfile = tfiles[-1].replace("pmc_traffic.json", "pmc_counters.json")
+                if os.path.exists(cfile):
+                    ck = tl["kernel"].replace("conv3x3_split3<", "conv<").replace(" ", "")
+                    cv = json.load(open(cfile)).get(ck)
+                    if cv and cv.get("GRBM_GUI_ACTIVE") and cv.get("dur_us"):
+                        clk = cv["GRBM_GUI_ACTIVE"] / 8 / (cv["dur_us"] * 1e3)
+                        roofline["pmc_counters_source"] = os.path.relpath(cfile, ROOT)
+                        roofline["clock_ghz_held"] = round(clk, 3)
+                        roofline["mfma_busy"] = round(cv["SQ_VALU_MFMA_BUSY_CYCLES"] / 1024 / (cv["GRBM_GUI_ACTIVE"] / 8), 4)
+                        roofline["frac_at_held_clock"] = round(roofline["frac"] * 2.4 / clk, 4)
             else:       # measured on another build (or not this kernel): never quote stale bytes
                 roofline["traffic_note"] = ("no PMC traffic of this build's " + dom_name + " kernel in "
                                             + roofline["traffic_source"])
