@@ -191,7 +191,8 @@ int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, i
  * A training frame runs cista_forward_train, which also fills a `saved` buffer with the
  * activations the backward needs; cista_backward then takes the gradients of the frame's five
  * outputs and returns the gradients of its inputs (previous image and states: BPTT) and of
- * all 25 parameters.  Both require base_channels in {32, 64}. */
+ * all 25 parameters.  Both require base_channels % 32 == 0 and base_channels <= 256 (the
+ * wgrad partial-sum buffer holds the gates conv's 4C x 3C x 9 block). */
 size_t cista_saved_bytes(const cista_config *cfg, int B, int H, int W);
 size_t cista_train_workspace_bytes(const cista_config *cfg, int B, int H, int W);
 int cista_forward_train(const cista_config *cfg, const void *packed, int B, int H, int W,

@@ -197,7 +197,8 @@ def test_dark_frames_elementwise_vs_fp64():
 
 # ------------------------------------------------------------------ oracle on seeded inputs
 @pytest.mark.parametrize("C,depth,B,H,W", [(64, 5, 3, 36, 52), (64, 3, 2, 18, 30),
-                                           (32, 1, 1, 4, 4), (64, 5, 1, 6, 8), (32, 2, 2, 50, 26)])
+                                           (32, 1, 1, 4, 4), (64, 5, 1, 6, 8), (32, 2, 2, 50, 26),
+                                           (96, 2, 2, 20, 28), (128, 2, 1, 16, 24)])
 def test_oracle_random(C, depth, B, H, W):
     params = fx.stress_params(C, depth, 5, seed=100 + C + depth)
     vox = fx.synthetic_voxels(2, B, 5, H, W, n_events=max(8, fx.density_matched_events(H, W)),

@@ -272,3 +272,42 @@ def test_wgrad_tr_kernel_matches_fp64(xscale):
     # fp32 accumulation over 4680 pixels: ~sqrt(N) x 6e-8 of the largest entry
     assert rel_err(dW.double().cpu().numpy(), ref.cpu().numpy()) < 1e-5
     assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
+
+
+@pytest.mark.parametrize("H,W,C", [(6, 8, 32), (8, 12, 32), (12, 10, 32), (12, 16, 96), (10, 14, 128), (8, 8, 256)])
+def test_small_images_bptt_against_fp64_autograd(H, W, C):
+    """The dgrads fold the reflect padding in their epilogue (EPI_FOLD + fold_fix_kernel) when the
+    half-resolution input has rows 1 and n-2 distinct (h, w >= 4) and take the padded-domain
+    dgrad + fold_reflect_kernel pass otherwise: 6x8 (h = 3, the pass), 8x12 (h = 4, the smallest
+    epilogue fold, every border row and column a reflected one) and 12x10 (w = 5).  Two-frame
+    BPTT (prev_img = output.clone(), states carried, L1 on the last frame) against fp64 autograd
+    through the PyTorch-CPU restatement of the reference forward.  C = 96, 128 and 256 (the largest training supports) cover the
+    training path beyond the reference default's channel counts (any multiple of 32)."""
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU
+    depth, B = 2, 2
+    params = fx.stress_params(C, depth, 5, seed=H * 100 + W, lam=0.05)
+    m = CistaLSTCNet([H, W], base_channels=C, depth=depth, num_bins=5)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, depth)
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    rng = np.random.default_rng(H * W)
+    vox = rng.standard_normal((2, B, 5, H, W)).astype(np.float32)
+    target = rng.random((B, 1, H, W)).astype(np.float32)
+    prev, state = torch.zeros(B, 1, H, W, device=DEV), None
+    for f in range(2):
+        out, state = m(gpu(vox[f]), prev, state)
+        prev = out.clone()
+    torch.nn.functional.l1_loss(out, gpu(target)).backward()
+    torch.cuda.synchronize()
+    o = CistaLSTCTorchCPU(params, depth, dtype=torch.float64, requires_grad=True)
+    prev_t, st_t = torch.zeros(B, 1, H, W, dtype=torch.float64), None
+    for f in range(2):
+        out_t, st_t = o.forward_grad(torch.from_numpy(vox[f]).double(), prev_t, st_t)
+        prev_t = out_t.clone()
+    torch.nn.functional.l1_loss(out_t, torch.from_numpy(target).double()).backward()
+    bad = {}
+    for k, g in grads_by_name(m).items():
+        e = rel_err(g, o.p[k].grad.numpy())
+        if not e < GTOL:
+            bad[k] = e
+    assert not bad, bad

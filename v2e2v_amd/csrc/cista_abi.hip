@@ -387,14 +387,14 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         } else {
             if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4, 2, PS>(a, st);
             if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4, 2, PS>(a, st);
-            if (a.N == 32) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N % 32 == 0) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);   // N = 32, 96, 160 ...
         }
         return CISTA_ERR_UNSUPPORTED;
     } else if constexpr (CISTA_VARIANT >= 1 && G <= 2) {
         constexpr int MT = CISTA_PF_MT;
         if (a.N % 128 == 0) return launch_conv_cfg<MT, 2, 1, 4, STAGE, EPI, G, true>(a, st);
-        if (a.N == 64) return launch_conv_cfg<MT, 2, 2, 2, STAGE, EPI, G, true>(a, st);
-        if (a.N == 32) return launch_conv_cfg<MT, 2, 4, 1, STAGE, EPI, G, true>(a, st);
+        if (a.N % 64 == 0) return launch_conv_cfg<MT, 2, 2, 2, STAGE, EPI, G, true>(a, st);
+        if (a.N % 32 == 0) return launch_conv_cfg<MT, 2, 4, 1, STAGE, EPI, G, true>(a, st);
         return CISTA_ERR_UNSUPPORTED;
     } else {
         if (a.N >= 256 && a.N % 256 == 0) return launch_conv_cfg<8, 4, 1, 4, STAGE, EPI, G>(a, st);
@@ -473,6 +473,7 @@ struct Frame {
 #ifndef CISTA_FUSED_IN
 #define CISTA_FUSED_IN 1
 #endif
+constexpr size_t IN_TILE_LDS = 160 * 1024;   // input-stage transpose tiles (LDS per workgroup)
 inline bool fused_input(const cista_config &cfg) { return CISTA_FUSED_IN && cfg.num_bins <= 8; }
 #ifndef CISTA_S2D_IN
 #define CISTA_S2D_IN 1
@@ -576,9 +577,11 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                     }
                     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
                 }
-                const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9,
-                              fa.border_only ? C / 32 : 1);
-                const size_t lds = (size_t)256 * (C + 1) * 4;
+                // channel split: C / 32 ways for the border pass, else as few as fit the LDS
+                int zs = fa.border_only ? C / 32 : 1;
+                while (!fa.border_only && ((C / 32) % zs || (size_t)256 * (C / zs + 1) * 4 > IN_TILE_LDS)) ++zs;
+                const dim3 g2((unsigned)((most + 255) / 256), fa.border_only ? 8 : 9, (unsigned)zs);
+                const size_t lds = (size_t)256 * (C / zs + 1) * 4;
                 switch (f.cfg->num_bins) {
 #define NBCASE(n)                                                                           \
     case n:                                                                                 \
@@ -596,8 +599,11 @@ int run_layer(const Frame &f, int layer, int it = 0) {
             ia.bias = blob<float>(f.packed, f.L.bIn);
             ia.out = f.full; ia.B = B; ia.H = f.H; ia.W = f.W; ia.nb = f.cfg->num_bins; ia.C = C;
             const long npix = (long)B * f.H * f.W;
-            const dim3 g1((unsigned)((npix + 255) / 256));
-            const size_t lds = (size_t)256 * (C + 1) * 4;
+            // channel split (large C): as few ways as keep the [256][2 CH + 1] tile in the LDS
+            int ys = 1;
+            while (((C / 32) % ys || (size_t)256 * (C / ys + 1) * 4 > IN_TILE_LDS)) ++ys;
+            const dim3 g1((unsigned)((npix + 255) / 256), (unsigned)ys);
+            const size_t lds = (size_t)256 * (C / ys + 1) * 4;
             switch (f.cfg->num_bins) {
 #define NBCASE(n)                                                                           \
     case n:                                                                                 \
@@ -693,6 +699,7 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 if (f.u) return launch_conv<STAGE_UP, EPI_UP_Q_SAVE, 1>(a, f.st);
                 return launch_conv<STAGE_UP, EPI_UP_Q, 1>(a, f.st);
             }
+            if (f.u) a.out0 = f.u;  // training: u itself is saved (final_stage_kernel reads it there)
             return launch_conv<STAGE_UP, EPI_RELU, 1>(a, f.st);
         case CISTA_LAYER_FINAL: {   // sigmoid(final_conv(u))                  e2v_model.py:87-88
             const long total = (long)B * f.H * f.W;
@@ -704,7 +711,7 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 hipLaunchKernelGGL(final_q_kernel, g1, dim3(256), 0, f.st, fq);
             } else {
                 FinalArgs fa;
-                fa.u = f.full; fa.w = blob<float>(f.packed, f.L.wF); fa.bias = blob<float>(f.packed, f.L.bF);
+                fa.u = f.u ? f.u : f.full; fa.w = blob<float>(f.packed, f.L.wF); fa.bias = blob<float>(f.packed, f.L.bF);
                 fa.rec = f.rec; fa.pre = f.pre; fa.B = B; fa.H = f.H; fa.W = f.W; fa.C = C;
                 hipLaunchKernelGGL(final_stage_kernel, g1, dim3(256), 0, f.st, fa);
             }
@@ -1202,6 +1209,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     const long hw = (long)B * h * w, HW = (long)B * H * W;
     BwdWs &ws = k.ws;
     hipStream_t st = k.st;
+    // the reflect fold in the dgrad epilogue (dgrad_fold) needs input rows 1 and n-2 distinct
+    // (n, m >= 4); smaller images take the padded-domain dgrad + fold_reflect_kernel pass
+    const bool fold_half = CISTA_FOLD_EPI && h >= 4 && w >= 4, fold_full = CISTA_FOLD_EPI && H >= 4 && W >= 4;
     // ---- 1-2. output stage: rec = sigmoid(final_conv(u)), u = relu(upsamp_conv(up(h))) --------
     CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
     if (g.g_rec) {
@@ -1231,7 +1241,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
         CHECK(side_join(k));                            // dxpF (its X) is overwritten next
         float *gup = ws.gU;                              // g wrt up(h)
-        if (CISTA_FOLD_EPI) {
+        if (fold_full) {
             gup = ws.dxpF;                               // (B, H, W, C): the dgrad's input gU is still read
             CHECK(dgrad_fold(k, CV_UP, ws.gU, gsu, fseg(gup, C, 0), fseg(nullptr, 0, 0), C));
         } else {
@@ -1254,7 +1264,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
-    if (CISTA_FOLD_EPI) {                                // relu(Dg) mask; h_prev's part if wanted
+    if (fold_half) {                                // relu(Dg) mask; h_prev's part if wanted
         CHECK(dgrad_fold(k, CV_LSTM, ws.Gl, gsc, fseg(ws.gy, C, 0, 1.0f, FOLD_MASK, const_cast<float *>(sv.y), scale_slots(k)),
                          fseg(io.h_prev ? g.g_h_prev : nullptr, C, 0), C));
     } else {
@@ -1267,7 +1277,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
-    if (CISTA_FOLD_EPI) {                                // g_z + fold
+    if (fold_half) {                                // g_z + fold
         CHECK(dgrad_fold(k, CV_DG, ws.gy, gsc, fseg(ws.gz, 2 * C, 0, 1.0f, g.g_z ? FOLD_ADD : FOLD_SET, const_cast<float *>(g.g_z)),
                          fseg(nullptr, 0, 0), 2 * C));
     } else {
@@ -1290,7 +1300,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     for (int it = D - 1; it >= 0; --it) {
         const float *v = sv.v + (size_t)it * hw * 2 * C;
         float *gv = ws.gv + (size_t)it * hw * 2 * C, *gxk = ws.gxk + (size_t)it * hw * C;
-        if (1024 % (2 * C) == 0)
+        if (2 * C <= 1024)
             hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
                                lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
         else
@@ -1300,7 +1310,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // P: v = z_k + P(x_k) + b_P
         gsc = scale_of(k, sclP + 2 * it);
         CHECK_PTR(gsc);
-        if (CISTA_FOLD_EPI) {                            // gx1 += too
+        if (fold_half) {                            // gx1 += too
             CHECK(dgrad_fold(k, CV_P, gv, gsc, fseg(gxk, C, 0, 1.0f, FOLD_DST2, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
         } else {
             CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
@@ -1309,7 +1319,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
         gsc = scale_of(k, sclD + 2 * it);
         CHECK_PTR(gsc);
-        if (CISTA_FOLD_EPI) {                            // identity path + fold
+        if (fold_half) {                            // identity path + fold
             CHECK(dgrad_fold(k, CV_D, gxk, gsc, fseg(ws.gz, 2 * C, 0, -1.0f, FOLD_ADD, gv), fseg(nullptr, 0, 0), 2 * C));
         } else {
             CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
@@ -1344,7 +1354,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
     const bool want_zp = io.z_prev && g.g_z_prev;
-    if (CISTA_FOLD_EPI) {                                // gz0 is final here: its slot set follows Gl's
+    if (fold_half) {                                // gz0 is final here: its slot set follows Gl's
         CHECK(dgrad_fold(k, CV_OUTG, ws.Go, gsc, fseg(ws.gz0, 2 * C, 0, 1.0f, FOLD_ADD, ws.gz0, scale_slots(k, 1)),
                          fseg(want_zp ? g.g_z_prev : nullptr, 2 * C, 0), 2 * C));
     } else {
@@ -1358,7 +1368,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
-    if (CISTA_FOLD_EPI) {
+    if (fold_half) {
         CHECK(dgrad_fold(k, CV_GATES, ws.Gl, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1),
                          fseg(want_zp ? g.g_z_prev : nullptr, 2 * C, 0, 1.0f, FOLD_ADD, want_zp ? g.g_z_prev : nullptr), C));
     } else {
@@ -1370,7 +1380,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK_PTR(gsc);
     CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
-    if (CISTA_FOLD_EPI) {
+    if (fold_half) {
         CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
     } else {
         CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
@@ -1756,7 +1766,7 @@ size_t cista_train_workspace_bytes(const cista_config *cfg, int B, int H, int W)
 }
 
 static int train_supported(const cista_config *cfg) {
-    return (cfg->base_channels == 64 || cfg->base_channels == 32) ? CISTA_OK : CISTA_ERR_UNSUPPORTED;
+    return (cfg->base_channels % 32 == 0 && cfg->base_channels <= 256) ? CISTA_OK : CISTA_ERR_UNSUPPORTED;
 }
 
 // the backward's dominant launch on its own (timing / PMC hook): the tied ISTA P weight

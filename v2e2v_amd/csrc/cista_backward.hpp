@@ -1611,18 +1611,18 @@ __global__ void lstm_bwd_kernel(const float *gates, const float *c, const float 
 // softshrink backward (reference base_layers.py:11-12): z = relu(v-l) - relu(-v-l)
 // gv = gz * ([v > l] + [v < -l]);  dl_partial[block][c] = sum gz * (-[v > l] + [v < -l]).
 // Thread -> (pixel, channel) with a grid stride that is a multiple of C (fixed channel per
-// thread; requires 256 % C == 0), coalesced over channels.
+// thread: the first (256 / C) * C threads of a workgroup work; C <= 256), coalesced over channels.
 __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, const float *v,
                                                              const float *lam, float *gv,
                                                              float *dl_partial, long npix, int C,
                                                              unsigned *amax) {
     __shared__ float red[256];
     float mx = 0.0f;
-    const int c = threadIdx.x % C;
+    const int c = threadIdx.x % C, nl = (256 / C) * C;
     const float l = lam[c];
     const long total = npix * C;
     float acc = 0.0f;
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    for (long i = (long)blockIdx.x * nl + threadIdx.x; (int)threadIdx.x < nl && i < total; i += (long)gridDim.x * nl) {
         const float vv = v[i], g = gz[i];
         const bool up = vv > l, dn = vv < -l;
         gv[i] = g * ((up ? 1.0f : 0.0f) + (dn ? 1.0f : 0.0f));
@@ -1633,21 +1633,22 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
     __syncthreads();
     if ((int)threadIdx.x < C) {
         float s = 0.0f;
-        for (int k = threadIdx.x; k < 256; k += C) s += red[k];
+        for (int k = threadIdx.x; k < nl; k += C) s += red[k];
         dl_partial[(size_t)blockIdx.x * C + threadIdx.x] = s;
     }
     if (amax) amax_publish(amax, mx);
 }
 
-// softshrink_bwd_kernel over float4 channel groups (1024 % C == 0): the same gv and, per
-// workgroup, the same dlambda partials up to the order of the per-channel sums
+// softshrink_bwd_kernel over float4 channel groups (C % 4 == 0, C <= 1024): the same gv and, per
+// workgroup, the same dlambda partials up to the order of the per-channel sums.  The first
+// (256 / (C/4)) * (C/4) threads work (all 256 when 1024 % C == 0).
 __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, const float *v,
                                                               const float *lam, float *gv,
                                                               float *dl_partial, long npix, int C,
                                                               unsigned *amax) {
     __shared__ float4 red[256];
     float mx = 0.0f;
-    const int cq = C >> 2, c = (threadIdx.x % cq) * 4;
+    const int cq = C >> 2, c = (threadIdx.x % cq) * 4, nl = (256 / cq) * cq;
     const float4 l = *reinterpret_cast<const float4 *>(lam + c);
     const long total = npix * cq;
     const float4 *v4 = reinterpret_cast<const float4 *>(v), *g4 = reinterpret_cast<const float4 *>(gz);
@@ -1658,7 +1659,7 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
         a += g * ((dn ? 1.0f : 0.0f) - (up ? 1.0f : 0.0f));
         return g * ((up ? 1.0f : 0.0f) + (dn ? 1.0f : 0.0f));
     };
-    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < total; i += (long)gridDim.x * 256) {
+    for (long i = (long)blockIdx.x * nl + threadIdx.x; (int)threadIdx.x < nl && i < total; i += (long)gridDim.x * nl) {
         const float4 vv = v4[i], g = g4[i];
         float4 r;
         r.x = one(vv.x, g.x, l.x, acc.x);
@@ -1672,7 +1673,7 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
     __syncthreads();
     if ((int)threadIdx.x < cq) {
         float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
-        for (int k = threadIdx.x; k < 256; k += cq) {
+        for (int k = threadIdx.x; k < nl; k += cq) {
             s.x += red[k].x; s.y += red[k].y; s.z += red[k].z; s.w += red[k].w;
         }
         *reinterpret_cast<float4 *>(dl_partial + (size_t)blockIdx.x * C + 4 * threadIdx.x) = s;

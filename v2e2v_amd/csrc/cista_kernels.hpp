@@ -1647,10 +1647,12 @@ __global__ __launch_bounds__(256) void input_stage_kernel(const InputArgs a) {
 // flattened (b, y, x) index; its 9*(NB+1) reflect-padded inputs live in registers, the weights
 // are wave-uniform (scalar loads, SGPR operands), and the 256 x C outputs -- one contiguous
 // 256*C*4-byte run of the NHWC tensor -- leave through an LDS transpose as coalesced float4s.
+// gridDim.y > 1 (large C, whose 256 x C tile would not fit the LDS): workgroup y computes
+// channels [y CH, (y+1) CH) of each half (CH = C / 2 / gridDim.y) and stores two runs per pixel.
 template <int NB>
 __global__ __launch_bounds__(256) void input_stage_kernel_nb(const InputArgs a) {
-    extern __shared__ float tile[];           // [256][C + 1]
-    const int C = a.C, half = C / 2, ld = C + 1;
+    extern __shared__ float tile[];           // [256][2 CH + 1]
+    const int C = a.C, half = C / 2, CH = half / (int)gridDim.y, hbeg = (int)blockIdx.y * CH, ld = 2 * CH + 1;
     const long total = (long)a.B * a.H * a.W;
     const long pix0 = (long)blockIdx.x * 256;
     const long pix = pix0 + threadIdx.x;
@@ -1672,7 +1674,7 @@ __global__ __launch_bounds__(256) void input_stage_kernel_nb(const InputArgs a) 
 #pragma unroll
     for (int t = 0; t < 9; ++t) im[t] = a.prev[(size_t)b * plane + off[t]];
     float *row = tile + threadIdx.x * ld;
-    for (int c0 = 0; c0 < half; c0 += 16) {
+    for (int c0 = hbeg; c0 < hbeg + CH; c0 += 16) {
         float acc[16], acc2[16];
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
@@ -1693,19 +1695,30 @@ __global__ __launch_bounds__(256) void input_stage_kernel_nb(const InputArgs a) 
         }
 #pragma unroll
         for (int i = 0; i < 16; ++i) {
-            row[c0 + i] = acc[i];
-            row[half + c0 + i] = acc2[i];
+            row[c0 - hbeg + i] = acc[i];
+            row[CH + c0 - hbeg + i] = acc2[i];
         }
     }
     __syncthreads();
     const long nvalid = (total - pix0) < 256 ? (total - pix0) : 256;
-    const int nf4 = (int)(nvalid * C / 4);
-    float4 *dst = (float4 *)(a.out + (size_t)pix0 * C);
-    for (int i = threadIdx.x; i < nf4; i += 256) {
-        const int e = i * 4;
-        const int p = e / C, c = e - p * C;
-        const float *srow = tile + p * ld + c;
-        dst[i] = make_float4(srow[0], srow[1], srow[2], srow[3]);
+    if (gridDim.y == 1) {
+        const int nf4 = (int)(nvalid * C / 4);
+        float4 *dst = (float4 *)(a.out + (size_t)pix0 * C);
+        for (int i = threadIdx.x; i < nf4; i += 256) {
+            const int e = i * 4;
+            const int p = e / C, c = e - p * C;
+            const float *srow = tile + p * ld + c;
+            dst[i] = make_float4(srow[0], srow[1], srow[2], srow[3]);
+        }
+    } else {
+        const int nf4 = (int)(nvalid * 2 * CH / 4);
+        for (int i = threadIdx.x; i < nf4; i += 256) {
+            const int e = i * 4;
+            const int p = e / (2 * CH), c = e - p * 2 * CH;
+            const int ch = c < CH ? hbeg + c : half + hbeg + (c - CH);
+            const float *srow = tile + p * ld + c;
+            *(float4 *)(a.out + (size_t)(pix0 + p) * C + ch) = make_float4(srow[0], srow[1], srow[2], srow[3]);
+        }
     }
 }
 
@@ -1797,12 +1810,13 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
     const int b = (int)(pc / ((long)nr * nc));
     const size_t plane = (size_t)a.H * a.W;
     const float *ev = a.events + (size_t)b * NB * plane, *im = a.prev + (size_t)b * plane;
-    const int C = a.C, ld = C + 1;
+    const int C = a.C;
     const float *E = a.E + (size_t)cls * K * C;
-    float *row = tile + threadIdx.x * ld;
     // 32 output channels per pass; the window's inputs are re-read per pass (L1-resident);
-    // gridDim.z splits the channels over workgroups (the border pass has few pixels)
-    const int qn = C / gridDim.z, qbeg = blockIdx.z * qn;
+    // gridDim.z splits the channels over workgroups (the border pass has few pixels; large C,
+    // whose 256 x C tile would not fit the LDS); the tile holds this workgroup's qn channels
+    const int qn = C / gridDim.z, qbeg = blockIdx.z * qn, ld = qn + 1;
+    float *row = tile + threadIdx.x * ld;
     for (int q0 = qbeg; q0 < qbeg + qn; q0 += 32) {
         float acc[32];
 #pragma unroll
@@ -1822,7 +1836,7 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
                 for (int i = 0; i < 32; ++i) acc[i] = fmaf(v[ci], wt[(size_t)ci * C + i], acc[i]);
         }
 #pragma unroll
-        for (int i = 0; i < 32; ++i) row[q0 + i] = acc[i];
+        for (int i = 0; i < 32; ++i) row[q0 - qbeg + i] = acc[i];
     }
     __syncthreads();
     const int nvalid = (int)((total - p0) < 256 ? (total - p0) : 256);
@@ -1831,7 +1845,7 @@ __global__ __launch_bounds__(256) void input_w0_kernel(const FusedInArgs a) {
         const int p = i / q4, c = qbeg + (i - p * q4) * 4;
         const long pp = p0 + p;
         const int y = r0 + (int)((pp / nc) % nr), x = c0 + (int)(pp % nc), bb = (int)(pp / ((long)nr * nc));
-        const float *srow = tile + p * ld + c;
+        const float *srow = tile + p * ld + (c - qbeg);
         *(float4 *)(a.out + (((size_t)bb * a.h + y) * a.w + x) * C + c) = make_float4(srow[0], srow[1], srow[2], srow[3]);
     }
 }
