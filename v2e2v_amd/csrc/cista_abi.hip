@@ -1468,6 +1468,11 @@ int cista_debug_set_stamps(void *buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(cista::g_cista_stamps), &buf, sizeof(buf)) == hipSuccess ? CISTA_OK
                                                                                             : CISTA_ERR_HIP;
 }
+// ... and wgrad_tr_kernel's (scripts/wgrad_stamps.py)
+int cista_debug_set_wstamps(void *buf) {
+    return hipMemcpyToSymbol(HIP_SYMBOL(cista::g_cista_wstamps), &buf, sizeof(buf)) == hipSuccess ? CISTA_OK
+                                                                                             : CISTA_ERR_HIP;
+}
 #endif
 
 const char *cista_status_string(int s) {

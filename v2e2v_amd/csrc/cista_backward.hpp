@@ -780,6 +780,24 @@ __device__ __forceinline__ void split4(const float4 &v, uint2 &hi, uint2 &lo) {
                     __builtin_bit_cast(unsigned, __builtin_convertvector(r23, h2)));
 }
 
+// Diagnostic build only (CISTA_STAMPS=1, scripts/wgrad_stamps.py): lane 0 of wave 0 (MFMA) and
+// wave 4 (staging) records shader-clock timestamps into g_cista_wstamps[workgroup * 512 + role * 256
+// + slot].  MFMA wave: 0 start, 1 past the first barrier, 2 + 2 it MFMAs of tile it done, 3 + 2 it
+// past its barrier (it < 120), 250 MFMA loop done, 251 partials stored, 252 / 253 constant-rate
+// clock at start / end.  Staging wave: 0 start, 1 first tile committed, 2 past the first barrier,
+// 3 + 3 it next tile committed, 4 + 3 it its successor's loads issued, 5 + 3 it past the barrier.
+#if CISTA_STAMPS
+__device__ unsigned long long *g_cista_wstamps;
+#define WT_STAMP(slot, v)                                                                           \
+    do {                                                                                            \
+        unsigned long long *_p = g_cista_wstamps;                                                   \
+        if (_p && lane == 0 && (wave & 3) == 0 && (slot) < 256)                                     \
+            _p[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 512 + (wave >> 2) * 256 + (slot)] = (v); \
+    } while (0)
+#else
+#define WT_STAMP(slot, v) do { } while (0)
+#endif
+
 __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     extern __shared__ u32x4 wsm4[];
     _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
@@ -887,12 +905,15 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     if (loader) {
         // the roles run separate loops with the same barrier sequence, so the loaders' staging
         // registers and the MFMA waves' accumulators are never live at the same time
+        WT_STAMP(0, __builtin_amdgcn_s_memtime());
         if ((int)blockIdx.y < ntiles) {
             load_tile(blockIdx.y);
             commit(sm, xfl);
+            WT_STAMP(1, __builtin_amdgcn_s_memtime());
             if ((int)blockIdx.y + a.nsplit < ntiles) load_tile(blockIdx.y + a.nsplit);
         }
         __syncthreads();
+        WT_STAMP(2, __builtin_amdgcn_s_memtime());
         int it = 0;
         for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
             const int bi = it & 1;
@@ -917,9 +938,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
             if (tile + a.nsplit < ntiles) {
                 // the other buffer was last read before the barrier that opened this iteration
                 commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1));
+                WT_STAMP(3 + 3 * it, __builtin_amdgcn_s_memtime());
                 if (tile + 2 * a.nsplit < ntiles) load_tile(tile + 2 * a.nsplit);
+                WT_STAMP(4 + 3 * it, __builtin_amdgcn_s_memtime());
             }
             __syncthreads();
+            WT_STAMP(5 + 3 * it, __builtin_amdgcn_s_memtime());
         }
         if (do_bias) {
             reinterpret_cast<float4 *>(wsm4)[tid - 256] = bsum;
@@ -933,7 +957,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
     f32x4 acc[2][2][9];
     acc_zero(acc);
+    WT_STAMP(0, __builtin_amdgcn_s_memtime());
+    WT_STAMP(252, __builtin_amdgcn_s_memrealtime());
     __syncthreads();
+    WT_STAMP(1, __builtin_amdgcn_s_memtime());
     int it = 0;
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
         const int bi = it & 1;
@@ -989,8 +1016,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 }
             __builtin_amdgcn_sched_barrier(0);
         }
+        if (it < 120) WT_STAMP(2 + 2 * it, __builtin_amdgcn_s_memtime());
         __syncthreads();
+        if (it < 120) WT_STAMP(3 + 2 * it, __builtin_amdgcn_s_memtime());
     }
+    WT_STAMP(250, __builtin_amdgcn_s_memtime());
     if (do_bias) {
         // loader sums of co quad 16 sb + 4 sq -> per-co sums in a fixed order (waves, then sp)
         __syncthreads();
@@ -1019,6 +1049,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 for (int t = 0; t < 9; ++t) part[((size_t)co * a.Cin + ci) * 9 + t] = acc[u][v][t][j] * inv;
             }
     }
+    WT_STAMP(251, __builtin_amdgcn_s_memtime());
+    WT_STAMP(253, __builtin_amdgcn_s_memrealtime());
 }
 
 // --------------------------------------------------------------------------------------------
