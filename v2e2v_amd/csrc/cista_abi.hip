@@ -1004,6 +1004,9 @@ void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, flo
 #ifndef CISTA_WGRAD_TR
 #define CISTA_WGRAD_TR 1      // split-f16 wgrads on wgrad_tr_kernel (0: wgrad_split_kernel, A/B builds)
 #endif
+#ifndef CISTA_WGRAD_TR_S2
+#define CISTA_WGRAD_TR_S2 1   // W0's stride-2 wgrad on wgrad_tr_kernel<XS_S2> (0: exact fp32-MFMA wgrad_kernel)
+#endif
 constexpr int NCU = 256;      // MI355X compute units (8 XCDs x 32)
 
 // dW (+)= sign * wgrad ; G channels [Goff, Goff+Cout) of a Gc-channel NHWC tensor; and, when
@@ -1022,6 +1025,31 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     a.Cout = Cout; a.Cin = Cin;
     a.partial = k.ws.part;
     a.bpartial = db ? k.ws.bpart : nullptr;
+    constexpr bool TR_S2 = XS == XS_S2 && CISTA_WGRAD_TR_S2;
+    if (TR_S2 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 && Goff % 4 == 0 && x0c % 32 == 0 &&
+        x1c % 32 == 0 && Hin == 2 * Hout && Win == 2 * Wout) {
+        // W0 (stride 2): the split-f16 wgrad on 2 x 16-pixel tiles over a parity-split halo
+        if constexpr (TR_S2) {
+            using GE = WtGeo<XS_S2>;
+            a.gscale = gsc;
+            a.TH = GE::TH; a.TW = 16;
+            a.tiles_y = (Hout + GE::TH - 1) / GE::TH;
+            a.tiles_x = (Wout + 15) / 16;
+            const int ntiles = a.B * a.tiles_y * a.tiles_x;
+            const int nblk = (Cout / 64) * ((Cin + 63) / 64);
+            int ns = NCU / nblk;
+            const int lim = (int)(((long)WG_BLOCKS * 32 * 32) / ((long)Cout * Cin));
+            ns = ns > lim ? lim : ns;
+            ns = ns > ntiles ? ntiles : ns;
+            ns = ns < 1 ? 1 : ns;
+            ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
+            a.nsplit = ns;
+            if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S2>)) return CISTA_ERR_HIP;
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S2>, dim3(nblk, ns), dim3(512), GE::LDS, k.wst, a);
+            reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
+            return hip_ok();
+        }
+    }
     if (CISTA_WGRAD_SPLIT && XS == XS_S1 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 &&
         Goff % 4 == 0 && x0c % 32 == 0 && x1c % 32 == 0 && Hin == Hout && Win == Wout) {
         a.gscale = gsc;
@@ -1030,6 +1058,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.tiles_x = (Wout + WS_TW - 1) / WS_TW;
         const int ntiles = a.B * a.tiles_y * a.tiles_x;
         if (CISTA_WGRAD_TR) {
+            static_assert(WtGeo<XS_S1>::TH == WS_TH && WS_TW == 16, "wgrad_tr_kernel tiles");
             // 64 x 64 blocks, one 8-wave workgroup per CU: splits fill the CUs once (and fit
             // the partial buffer: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9)
             const int nblk = (Cout / 64) * ((Cin + 63) / 64);
@@ -1040,8 +1069,8 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = ns < 1 ? 1 : ns;
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
-            if (!allow_big_lds((const void *)wgrad_tr_kernel)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel, dim3(nblk, ns), dim3(512), WT_LDS, k.wst, a);
+            if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S1>)) return CISTA_ERR_HIP;
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S1>, dim3(nblk, ns), dim3(512), WtGeo<XS_S1>::LDS, k.wst, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }
@@ -1399,7 +1428,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         CHECK(run_layer(f, CISTA_LAYER_INPUT));
     }
     CHECK(side_fork(k));
-    CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b));
+    CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b, gsx));
     {
         // padded-domain stride-2 dgrad into dxpF (split-f16 MFMA, the four output phases of a
         // G pixel as one 4C-column conv over G, pack_w0phase_kernel), then reflect-fold into gxfull

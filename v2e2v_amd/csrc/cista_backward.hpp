@@ -747,11 +747,33 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
 //    the fp16 hi part (>= 32768 after the scale in force) is re-staged with a smaller power-of-two
 //    pre-scale sx and the accumulators are rescaled exactly (rare path, uniform per workgroup).
 // --------------------------------------------------------------------------------------------
-constexpr int WT_NPX = 96, WT_HW = 18, WT_HP = 144;
-constexpr int WT_GPL = WT_NPX * 16;                 // halves per G plane (part, 16-co block)
-constexpr int WT_XPL = WT_HP * 16;                  // halves per X plane (part, 16-ci block)
-constexpr int WT_BUF = 8 * WT_GPL + 8 * WT_XPL;     // halves per buffer: G planes [2][4], X [2][4]
-constexpr size_t WT_LDS = (size_t)2 * WT_BUF * 2 + 16 * 4;      // + maxima, flags, scale
+// Tile geometry per input stage.  Stride 1: 6 x 16 output pixels (3 K-steps), reflect-padded
+// 8 x 18 input halo.  Stride 2 (W0): 2 x 16 output pixels (1 K-step) over a 5 x 33 input halo
+// whose columns are stored parity-split (the 17 even columns, then the 16 odd ones), so the
+// input columns 2x + dx - 1 of four consecutive output pixels are four consecutive LDS pixels.
+template <int XS> struct WtGeo {
+    static constexpr int S = XS == XS_S2 ? 2 : 1;
+    static constexpr int TH = S == 2 ? 2 : 6;           // output rows per tile (x 16 columns)
+    static constexpr int NPX = TH * 16;                 // output pixels per tile
+    static constexpr int KS = NPX / 32;                 // 32-pixel K-steps per tile
+    static constexpr int HR = (TH - 1) * S + 3;         // halo rows
+    static constexpr int HW = 15 * S + 3;               // halo columns (= LDS row pitch in pixels)
+    static constexpr int HP = HR * HW;                  // halo pixels
+    static constexpr int UG = NPX / 16, UX = (HP + 15) / 16;   // staging items per loader lane
+    static constexpr int GPL = NPX * 16;                // halves per G plane (part, 16-co block)
+    static constexpr int XPL = HP * 16;                 // halves per X plane (part, 16-ci block)
+    static constexpr int BUF = 8 * GPL + 8 * XPL;       // halves per buffer: G planes [2][4], X [2][4]
+    static constexpr size_t LDS = (size_t)2 * BUF * 2 + 16 * 4;   // + maxima, flags, scale
+    // LDS pixel of halo pixel (hy, hx)
+    static __device__ __forceinline__ int xpos(int hy, int hx) {
+        return hy * HW + (S == 1 ? hx : (hx & 1) * 17 + (hx >> 1));
+    }
+    // LDS pixel read by K row r (0, 1) of K-step s, tap (dy, dx), column offset c (0..15)
+    static __device__ __forceinline__ int kpos(int s, int r, int dy, int dx, int c) {
+        return S == 1 ? (2 * s + r + dy) * HW + c + dx : (4 * s + 2 * r + dy) * HW + (dx & 1) * 17 + (dx >> 1) + c;
+    }
+};
+static_assert(WtGeo<XS_S1>::HP == 144 && WtGeo<XS_S2>::HP == 165, "wgrad_tr halo geometry");
 
 typedef short s16x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) s16x4 lds_s16x4;
@@ -798,7 +820,10 @@ __device__ unsigned long long *g_cista_wstamps;
 #define WT_STAMP(slot, v) do { } while (0)
 #endif
 
+template <int XS>
 __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
+    using GE = WtGeo<XS>;
+    constexpr int WT_GPL = GE::GPL, WT_XPL = GE::XPL, WT_BUF = GE::BUF;
     extern __shared__ u32x4 wsm4[];
     _Float16 *sm = reinterpret_cast<_Float16 *>(wsm4);
     float *xmx = reinterpret_cast<float *>(sm + 2 * WT_BUF);     // [4] loader X maxima (rare path)
@@ -816,27 +841,28 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
     const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
-    float4 gv[6], xv[9];
+    float4 gv[GE::UG], xv[GE::UX];
     auto tile_origin = [&](int tile, int &b, int &oy0, int &ox0) __attribute__((always_inline)) {
         int tt = tile;
         const int tx = tt % a.tiles_x;
         tt /= a.tiles_x;
         const int ty = tt % a.tiles_y;
         b = tt / a.tiles_y;
-        oy0 = ty * 6;
+        oy0 = ty * GE::TH;
         ox0 = tx * 16;
     };
     auto load_x = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
-        const int hp = 4 * (lw + 4 * u) + sp;                            // 0..143
-        const int hy = hp / WT_HW, hx = hp - hy * WT_HW;
-        return wg_load_x4<XS_S1>(a, b, oy0 - 1 + hy, ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
+        const int hp = 4 * (lw + 4 * u) + sp;                            // 0..HP-1 (+ masked)
+        const int hy = hp / GE::HW, hx = hp - hy * GE::HW;
+        if (GE::HP % 16 && hp >= GE::HP) return make_float4(0.f, 0.f, 0.f, 0.f);
+        return wg_load_x4<XS>(a, b, GE::S * oy0 - 1 + hy, GE::S * ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
     };
     auto load_tile = [&](int tile) __attribute__((always_inline)) {
         int b, oy0, ox0;
         tile_origin(tile, b, oy0, ox0);
 #pragma unroll
-        for (int u = 0; u < 6; ++u) {
-            const int p = 4 * (lw + 4 * u) + sp;                         // 0..95
+        for (int u = 0; u < GE::UG; ++u) {
+            const int p = 4 * (lw + 4 * u) + sp;                         // 0..NPX-1
             const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
             gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
             if (oy < a.Hout && ox < a.Wout)
@@ -844,21 +870,23 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                     a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
         }
 #pragma unroll
-        for (int u = 0; u < 9; ++u) xv[u] = load_x(b, oy0, ox0, u);
+        for (int u = 0; u < GE::UX; ++u) xv[u] = load_x(b, oy0, ox0, u);
     };
     auto put_x = [&](_Float16 *Xp, int u, float4 v) __attribute__((always_inline)) {
         const int hp = 4 * (lw + 4 * u) + sp;
+        if (GE::HP % 16 && hp >= GE::HP) return;
+        const int hy = hp / GE::HW, pos = GE::xpos(hy, hp - hy * GE::HW);
         if (__builtin_expect(sx != 1.0f, 0)) { v.x *= sx; v.y *= sx; v.z *= sx; v.w *= sx; }
         uint2 hi, lo;
         split4(v, hi, lo);
-        *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + hp * 16 + 4 * sq) = hi;
-        *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + hp * 16 + 4 * sq) = lo;
+        *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + pos * 16 + 4 * sq) = hi;
+        *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + pos * 16 + 4 * sq) = lo;
     };
     // registers -> LDS buffer (hi / lo planes); publishes whether this wave's X overflowed
     auto commit = [&](_Float16 *buf, int *flag) __attribute__((always_inline)) {
         _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
 #pragma unroll
-        for (int u = 0; u < 6; ++u) {
+        for (int u = 0; u < GE::UG; ++u) {
             const int p = 4 * (lw + 4 * u) + sp;
             if (do_bias) { bsum.x += gv[u].x; bsum.y += gv[u].y; bsum.z += gv[u].z; bsum.w += gv[u].w; }
             const float4 v = make_float4(gv[u].x * gsc, gv[u].y * gsc, gv[u].z * gsc, gv[u].w * gsc);
@@ -869,7 +897,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         }
         float m = 0.0f;
 #pragma unroll
-        for (int u = 0; u < 9; ++u) {
+        for (int u = 0; u < GE::UX; ++u) {
             m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
             put_x(Xp, u, xv[u]);
         }
@@ -923,7 +951,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 tile_origin(tile, b, oy0, ox0);
                 float m = 0.0f;
 #pragma unroll 1
-                for (int u = 0; u < 9; ++u) {
+                for (int u = 0; u < GE::UX; ++u) {
                     const float4 v = load_x(b, oy0, ox0, u);
                     m = fmaxf(m, fmaxf(fmaxf(fabsf(v.x), fabsf(v.y)), fmaxf(fabsf(v.z), fabsf(v.w))));
                 }
@@ -932,7 +960,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 __syncthreads();
                 new_scale();
 #pragma unroll 1
-                for (int u = 0; u < 9; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
+                for (int u = 0; u < GE::UX; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
                 __syncthreads();
             }
             if (tile + a.nsplit < ntiles) {
@@ -989,20 +1017,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         };
         auto read_x = [&](int s, int t, f16x8 (&xh)[2], f16x8 (&xl)[2]) __attribute__((always_inline)) {
             const int dy = t / 3, dx = t % 3;
+            constexpr int R1 = GE::S * GE::HW * 16;     // K row 1 (the next output row) in halves
 #pragma unroll
             for (int v = 0; v < 2; ++v) {
-                const int off = (pci + v) * WT_XPL + ((2 * s + dy) * WT_HW + 4 * kg + rq + dx) * 16 + 4 * rp;
-                xh[v] = cat_frag(tr_read(Xp, off), tr_read(Xp, off + WT_HW * 16));
-                xl[v] = cat_frag(tr_read(Xp, off + 4 * WT_XPL), tr_read(Xp, off + 4 * WT_XPL + WT_HW * 16));
+                const int off = (pci + v) * WT_XPL + GE::kpos(s, 0, dy, dx, 4 * kg + rq) * 16 + 4 * rp;
+                xh[v] = cat_frag(tr_read(Xp, off), tr_read(Xp, off + R1));
+                xl[v] = cat_frag(tr_read(Xp, off + 4 * WT_XPL), tr_read(Xp, off + 4 * WT_XPL + R1));
             }
         };
         f16x8 gh[2][2], gl[2][2], xh[2][2], xl[2][2];
         read_g(0, gh[0], gl[0]);
         read_x(0, 0, xh[0], xl[0]);
 #pragma unroll
-        for (int n = 0; n < 27; ++n) {
+        for (int n = 0; n < 9 * GE::KS; ++n) {
             const int s = n / 9, t = n % 9, xb = n & 1, gb = s & 1;
-            if (n + 1 < 27) {
+            if (n + 1 < 9 * GE::KS) {
                 read_x((n + 1) / 9, (n + 1) % 9, xh[xb ^ 1], xl[xb ^ 1]);
                 if (t == 8) read_g(s + 1, gh[gb ^ 1], gl[gb ^ 1]);
             }
