@@ -239,6 +239,14 @@ int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float
                        const float *gscale, float *dW, float *db, void *workspace,
                        size_t workspace_bytes, void *stream);
 
+/* Test / timing hook: W0's stride-2 weight gradient as cista_backward runs it (split-f16 wgrad
+ * over a parity-split halo + partial reduction).  G (B, H/2, W/2, C) and X (B, H, W, C) NHWC
+ * fp32, gscale {s, 1/s} of G, dW (C, C, 3, 3) and db (C) written.  workspace:
+ * cista_train_workspace_bytes. */
+int cista_wgrad_w0(const cista_config *cfg, int B, int H, int W, const float *G, const float *X,
+                   const float *gscale, float *dW, float *db, void *workspace, size_t workspace_bytes,
+                   void *stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -274,6 +274,37 @@ def test_wgrad_tr_kernel_matches_fp64(xscale):
     assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("xscale", [1.0, 3.0e5])
+def test_wgrad_tr_s2_kernel_matches_fp64(xscale):
+    """W0's stride-2 weight gradient (cista_wgrad_w0: wgrad_tr_kernel<XS_S2> over a parity-split
+    5 x 33 halo + reduce_partials_kernel) against an fp64 stride-2 conv weight gradient over the
+    reflect-padded input.  36 x 52 gives 18 x 26 outputs: ragged 2 x 16 tiles in x and the
+    reflected bottom / right halo rows; xscale = 3e5 sends every tile through the re-staging path."""
+    import ctypes
+    from v2e2v_amd import _lib
+    C, B, H, W = 64, 3, 36, 52
+    h, w = H // 2, W // 2
+    m = CistaLSTCNet([H, W], base_channels=C, depth=2, num_bins=5).to(DEV)
+    g = torch.Generator(device=DEV).manual_seed(6)
+    G = torch.rand(B, h, w, C, device=DEV, generator=g) * 2 - 1
+    X = (torch.rand(B, H, W, C, device=DEV, generator=g) * 2 - 1) * xscale
+    sc = torch.tensor([8192.0, 1.0 / 8192.0], device=DEV)
+    dW = torch.empty(C, C, 3, 3, device=DEV)
+    db = torch.empty(C, device=DEV)
+    ws = m.train_workspace(B, H, W, DEV)
+    L = _lib.lib()
+    cfg = m._cfg()
+    _lib.check(L.cista_wgrad_w0(ctypes.byref(cfg), B, H, W, G.data_ptr(), X.data_ptr(), sc.data_ptr(),
+                                dW.data_ptr(), db.data_ptr(), ws.data_ptr(), ws.numel(),
+                                torch.cuda.current_stream().cuda_stream), "cista_wgrad_w0")
+    torch.cuda.synchronize()
+    Gd = G.double().permute(0, 3, 1, 2)
+    Xd = torch.nn.functional.pad(X.double().permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect")
+    ref = torch.nn.grad.conv2d_weight(Xd, (C, C, 3, 3), Gd, stride=2)
+    assert rel_err(dW.double().cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("H,W,C", [(6, 8, 32), (8, 12, 32), (12, 10, 32), (12, 16, 96), (10, 14, 128), (8, 8, 256)])
 def test_small_images_bptt_against_fp64_autograd(H, W, C):
     """The dgrads fold the reflect padding in their epilogue (EPI_FOLD + fold_fix_kernel) when the

@@ -101,6 +101,8 @@ def _declare(lib):
                                    P(CistaParamGrads), c_void_p, c_size_t, c_void_p]),
         "cista_wgrad_ista_p": (c_int, [P(CistaConfig), c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
                                        c_void_p, c_void_p, c_size_t, c_void_p]),
+        "cista_wgrad_w0": (c_int, [P(CistaConfig), c_int, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p,
+                                   c_void_p, c_void_p, c_size_t, c_void_p]),
         "cista_launch_layer": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, c_int,
                                        P(CistaFrameIO), c_void_p, c_size_t, c_void_p]),
         "cista_sequence_capture": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO), c_int,

@@ -992,10 +992,50 @@ const float *scale_of(Bwd &k, float *dst) {
 }
 
 // dst (+)= sign * the split sum of the wgrad partials, and db from the bias partials, one launch
-void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, float sign, int accumulate) {
+void reduce_parts_at(Bwd &k, const float *part, const float *bpart, int ns, long n, float *dst, float *db, long nbias,
+                     float sign, int accumulate) {
     const long nb = db ? nbias : 0;
-    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.wst, (const float *)k.ws.part, ns, n,
-                       dst, sign, accumulate, (const float *)k.ws.bpart, nb, db);
+    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.wst, part, ns, n, dst, sign, accumulate,
+                       bpart, nb, db);
+}
+void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, float sign, int accumulate) {
+    reduce_parts_at(k, k.ws.part, k.ws.bpart, ns, n, dst, db, nbias, sign, accumulate);
+}
+
+#ifndef CISTA_WIN_NS
+#define CISTA_WIN_NS 512        // splits of the fused We / Wi wgrad (wgrad_in_kernel)
+#endif
+#ifndef CISTA_WGRAD_IN
+#define CISTA_WGRAD_IN 1   // We / Wi wgrads in one fp32-MFMA pass over gxfull (0: two wgrad_small_kernel launches)
+#endif
+// We and Wi weight / bias gradients from gxfull in one launch (wgrad_in_kernel); C in {32, 64},
+// num_bins <= 8.  Returns CISTA_ERR_UNSUPPORTED for other shapes (the caller falls back).
+int wgrad_inputs(Bwd &k, const float *gx, const float *ev, const float *img, const cista_param_grads &pg) {
+    const int C = k.C, nb = k.cfg->num_bins, half = C / 2;
+    if (!CISTA_WGRAD_IN || (C != 32 && C != 64) || nb < 1 || nb > 8) return CISTA_ERR_UNSUPPORTED;
+    WgradInArgs a;
+    a.G = gx; a.ev = ev; a.img = img;
+    a.B = k.B; a.H = k.H; a.W = k.W; a.C = C;
+    a.tiles_y = (k.H + 7) / 8;
+    a.tiles_x = (k.W + 15) / 16;
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    const int ns = ntiles < CISTA_WIN_NS ? ntiles : CISTA_WIN_NS;
+    a.nsplit = ns;
+    a.partE = k.ws.part;
+    a.partI = k.ws.part + (size_t)ns * half * nb * 9;
+    a.bpartE = k.ws.bpart;
+    a.bpartI = k.ws.bpart + (size_t)ns * half;
+    const size_t lds = ((size_t)WI_TP * (C + 16) + (size_t)(nb + 1) * WI_HPX) * 4;
+    switch (nb * 2 + (C == 64 ? 1 : 0)) {
+#define WICASE(n)                                                                                      \
+    case 2 * n: hipLaunchKernelGGL((wgrad_in_kernel<n, 1>), dim3(ns), dim3(256), lds, k.wst, a); break;              \
+    case 2 * n + 1: hipLaunchKernelGGL((wgrad_in_kernel<n, 2>), dim3(ns), dim3(256), lds, k.wst, a); break;
+        WICASE(1) WICASE(2) WICASE(3) WICASE(4) WICASE(5) WICASE(6) WICASE(7) WICASE(8)
+#undef WICASE
+    }
+    reduce_parts_at(k, a.partE, a.bpartE, ns, (long)half * nb * 9, pg.We_w, pg.We_b, half, 1.0f, 0);
+    reduce_parts_at(k, a.partI, a.bpartI, ns, (long)half * 9, pg.Wi_w, pg.Wi_b, half, 1.0f, 0);
+    return hip_ok();
 }
 
 #ifndef CISTA_WGRAD_SPLIT
@@ -1003,6 +1043,12 @@ void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, flo
 #endif
 #ifndef CISTA_WGRAD_TR
 #define CISTA_WGRAD_TR 1      // split-f16 wgrads on wgrad_tr_kernel (0: wgrad_split_kernel, A/B builds)
+#endif
+#ifndef CISTA_WSMALL_NS
+#define CISTA_WSMALL_NS 512     // splits of the We / Wi wgrads (wgrad_small_kernel)
+#endif
+#ifndef CISTA_WC1_NS
+#define CISTA_WC1_NS 2048       // splits x channel blocks of the final-conv wgrad (wgrad_c1_kernel; 512: 57 us, 2048: 45 us at B = 8)
 #endif
 #ifndef CISTA_WGRAD_TR_S2
 #define CISTA_WGRAD_TR_S2 1   // W0's stride-2 wgrad on wgrad_tr_kernel<XS_S2> (0: exact fp32-MFMA wgrad_kernel)
@@ -1091,7 +1137,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.tiles_y = (Hout + 15) / 16;
         a.tiles_x = (Wout + 15) / 16;
         const int ntiles = a.B * a.tiles_y * a.tiles_x;
-        const int ns = ntiles < 512 ? ntiles : 512;
+        const int ns = ntiles < CISTA_WSMALL_NS ? ntiles : CISTA_WSMALL_NS;
         a.nsplit = ns;
         switch (Cin) {
 #define WSCASE(n) \
@@ -1110,7 +1156,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.tiles_x = (Wout + 15) / 16;
         const int ncb = Cin / 32;
         const int ntiles = a.B * a.tiles_y * a.tiles_x;
-        int ns = 512 / ncb;
+        int ns = CISTA_WC1_NS / ncb;
         ns = ns > ntiles ? ntiles : ns;
         ns = ns < 1 ? 1 : ns;
         a.nsplit = ns;
@@ -1460,8 +1506,10 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     // ---- 8. We / Wi ----------------------------------------------------------------------------
     const int half = C / 2, nb = k.cfg->num_bins;
     CHECK(side_fork(k));
-    CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0, pg.We_b));
-    CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0,
+    const int rin = wgrad_inputs(k, gxfull, io.events, io.prev_image, pg);
+    if (rin != CISTA_ERR_UNSUPPORTED) CHECK(rin);
+    else CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0, pg.We_b));
+    if (rin == CISTA_ERR_UNSUPPORTED) CHECK(wgrad<XS_NCHW>(k, gxfull, C, half, half, io.prev_image, 1, nullptr, 0, 1, H, W, H, W, pg.Wi_w, 1.0f, 0,
                          pg.Wi_b));
     if (g.g_prev_image) {
         DgradSmallArgs d;
@@ -1823,6 +1871,25 @@ int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float
     const int C = k.C;
     return wgrad<XS_S1>(k, G, 2 * C, 0, 2 * C, X, C, nullptr, 0, C, k.h, k.w, k.h, k.w, dW, 1.0f, 0, db, gscale,
                         cfg->depth * B);
+}
+
+int cista_wgrad_w0(const cista_config *cfg, int B, int H, int W, const float *G, const float *X,
+                   const float *gscale, float *dW, float *db, void *workspace, size_t workspace_bytes,
+                   void *stream) {
+    if (!cfg_ok(cfg) || train_supported(cfg) != CISTA_OK) return CISTA_ERR_UNSUPPORTED;
+    if (!G || !X || !gscale || !dW || !db || !workspace || B <= 0) return CISTA_ERR_INVALID;
+    if ((H & 1) || (W & 1) || H < 4 || W < 4) return CISTA_ERR_INVALID;
+    Bwd k;
+    k.cfg = cfg; k.packed = nullptr; k.L = make_layout(*cfg);
+    k.B = B; k.H = H; k.W = W; k.h = H / 2; k.w = W / 2; k.C = cfg->base_channels;
+    k.st = static_cast<hipStream_t>(stream);
+    k.ws = carve_bwd(workspace, *cfg, B, H, W);
+    k.slot = 0;
+    k.pair = 0;
+    k.wst = k.st; k.evf = k.evj = nullptr;
+    if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
+    const int C = k.C;
+    return wgrad<XS_S2>(k, G, C, 0, C, X, C, nullptr, 0, C, H, W, k.h, k.w, dW, 1.0f, 0, db, gscale);
 }
 
 int cista_forward_train(const cista_config *cfg, const void *packed, int B, int H, int W,

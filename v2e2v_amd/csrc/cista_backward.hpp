@@ -1268,6 +1268,160 @@ __global__ __launch_bounds__(256) void wgrad_small_kernel(const WgradArgs a) {
     }
 }
 
+// --------------------------------------------------------------------------------------------
+// We and Wi weight (and bias) gradients in ONE pass over gxfull (B, H, W, C NHWC; was one
+// wgrad_small_kernel launch per half, each fetching the whole 256-B pixel rows for its 128 B):
+//   dWe[co][ci][t] = sum_P G(P, co) ev_pad(P + t, ci)        co < C/2, ci < NB
+//   dWi[co][t]     = sum_P G(P, C/2 + co) img_pad(P + t)
+// as pixel-reduction GEMMs on exact fp32 MFMA (v_mfma_f32_16x16x4f32): K = pixels of an 8 x 16
+// tile, M = output channel 16-blocks (MB = C/32 per half), N = im2col columns (plane, tap) read
+// straight from the reflect-padded (NB+1) x 10 x 18 input halo in LDS, plus a ones column whose
+// result is the bias gradient.  4 waves split each tile's 32 K-steps; the next tile's G / halo
+// loads are issued before this tile's MFMAs (registers); the waves' sums are added in a fixed
+// order at the end (deterministic), one partial per split ([split][co][n], reduce_partials_kernel).
+// --------------------------------------------------------------------------------------------
+struct WgradInArgs {
+    const float *G;            // gxfull (B, H, W, C)
+    const float *ev, *img;     // events (B, NB, H, W), previous image (B, 1, H, W)
+    float *partE, *partI;      // [nsplit][C/2][NB*9], [nsplit][C/2][9]
+    float *bpartE, *bpartI;    // [nsplit][C/2]
+    int B, H, W, C, tiles_x, tiles_y, nsplit;
+};
+constexpr int WI_TP = 128, WI_HR = 10, WI_HW = 18, WI_HPX = WI_HR * WI_HW;
+
+template <int NB, int MB>
+__global__ __launch_bounds__(256) void wgrad_in_kernel(const WgradInArgs a) {
+    constexpr int C = 32 * MB, HALF = 16 * MB, LDG = C + 16;   // LDG: lanes 0-15 / 16-31 on other banks
+    constexpr int NE = NB * 9 + 1, NBE = (NE + 15) / 16;        // E columns incl. the ones column
+    constexpr int GI = WI_TP * C / 4 / 256;                     // G float4 items per thread
+    constexpr int XI = ((NB + 1) * WI_HPX + 255) / 256;         // halo items per thread
+    extern __shared__ float wism[];
+    float *Gs = wism, *Xs = wism + WI_TP * LDG;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int ntiles = a.B * a.tiles_y * a.tiles_x;
+    // per-lane im2col offset of column n = 16 nb + (lane & 15): halo offset, -1 ones, -2 zero
+    int offE[NBE], offI;
+#pragma unroll
+    for (int nb = 0; nb < NBE; ++nb) {
+        const int n = nb * 16 + (lane & 15);
+        offE[nb] = n < NB * 9 ? (n / 9) * WI_HPX + ((n % 9) / 3) * WI_HW + (n % 3) : (n == NB * 9 ? -1 : -2);
+    }
+    {
+        const int n = lane & 15;
+        offI = n < 9 ? NB * WI_HPX + (n / 3) * WI_HW + (n % 3) : (n == 9 ? -1 : -2);
+    }
+    f32x4 accE[MB][NBE], accI[MB];
+#pragma unroll
+    for (int mb = 0; mb < MB; ++mb) {
+        accI[mb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int nb = 0; nb < NBE; ++nb) accE[mb][nb] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    float4 gv[GI];
+    float xv[XI];
+    auto load = [&](int tile) __attribute__((always_inline)) {
+        int tt = tile;
+        const int tx = tt % a.tiles_x;
+        tt /= a.tiles_x;
+        const int ty = tt % a.tiles_y;
+        const int b = tt / a.tiles_y;
+        const int oy0 = ty * 8, ox0 = tx * 16;
+#pragma unroll
+        for (int u = 0; u < GI; ++u) {
+            const int i = tid + u * 256;
+            const int p = i / (C / 4), c4 = i - p * (C / 4);
+            const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+            gv[u] = (oy < a.H && ox < a.W)
+                        ? *reinterpret_cast<const float4 *>(a.G + (((size_t)b * a.H + oy) * a.W + ox) * C + 4 * c4)
+                        : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+#pragma unroll
+        for (int u = 0; u < XI; ++u) {
+            const int i = tid + u * 256;
+            const int c = i / WI_HPX, hp = i - c * WI_HPX;
+            const int hy = hp / WI_HW, hx = hp - hy * WI_HW;
+            const int y = reflect_clamp(oy0 - 1 + hy, a.H), x = reflect_clamp(ox0 - 1 + hx, a.W);
+            xv[u] = i >= (NB + 1) * WI_HPX ? 0.0f
+                    : c < NB ? a.ev[(((size_t)b * NB + c) * a.H + y) * a.W + x]
+                             : a.img[((size_t)b * a.H + y) * a.W + x];
+        }
+    };
+    if ((int)blockIdx.x < ntiles) load(blockIdx.x);
+    for (int tile = blockIdx.x; tile < ntiles; tile += a.nsplit) {
+        __syncthreads();                                    // the previous tile's reads are done
+#pragma unroll
+        for (int u = 0; u < GI; ++u) {
+            const int i = tid + u * 256;
+            const int p = i / (C / 4), c4 = i - p * (C / 4);
+            *reinterpret_cast<float4 *>(Gs + p * LDG + 4 * c4) = gv[u];
+        }
+#pragma unroll
+        for (int u = 0; u < XI; ++u) {
+            const int i = tid + u * 256;
+            if (i < (NB + 1) * WI_HPX) Xs[i] = xv[u];
+        }
+        __syncthreads();
+        if (tile + a.nsplit < ntiles) load(tile + a.nsplit);
+#pragma unroll 2
+        for (int j = 0; j < WI_TP / 16; ++j) {
+            const int P = 4 * (wave + 4 * j) + (lane >> 4), base = (P >> 4) * WI_HW + (P & 15);
+            const float *gp = Gs + P * LDG + (lane & 15);
+            float bE[NBE];
+#pragma unroll
+            for (int nb = 0; nb < NBE; ++nb)
+                bE[nb] = offE[nb] >= 0 ? Xs[offE[nb] + base] : (offE[nb] == -1 ? 1.0f : 0.0f);
+            const float bI = offI >= 0 ? Xs[offI + base] : (offI == -1 ? 1.0f : 0.0f);
+#pragma unroll
+            for (int mb = 0; mb < MB; ++mb) {
+                const float aE = gp[mb * 16], aI = gp[HALF + mb * 16];
+#pragma unroll
+                for (int nb = 0; nb < NBE; ++nb)
+                    accE[mb][nb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aE, bE[nb], accE[mb][nb], 0, 0, 0);
+                accI[mb] = __builtin_amdgcn_mfma_f32_16x16x4f32(aI, bI, accI[mb], 0, 0, 0);
+            }
+        }
+    }
+    // waves 1..3 hand their sums to wave 0 through LDS, added in wave order
+    constexpr int NACC = MB * (NBE + 1) * 4;               // floats per lane
+    __syncthreads();
+    float *red = wism;                                      // [3][NACC][64]
+    if (wave > 0) {
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb) {
+#pragma unroll
+            for (int nb = 0; nb < NBE; ++nb)
+#pragma unroll
+                for (int r = 0; r < 4; ++r) red[((wave - 1) * NACC + (mb * (NBE + 1) + nb) * 4 + r) * 64 + lane] = accE[mb][nb][r];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) red[((wave - 1) * NACC + (mb * (NBE + 1) + NBE) * 4 + r) * 64 + lane] = accI[mb][r];
+        }
+    }
+    __syncthreads();
+    if (wave == 0) {
+        const int sp = blockIdx.x;
+#pragma unroll
+        for (int mb = 0; mb < MB; ++mb)
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int co = mb * 16 + 4 * (lane >> 4) + r;
+#pragma unroll
+                for (int nb = 0; nb <= NBE; ++nb) {
+                    float v = nb < NBE ? accE[mb][nb][r] : accI[mb][r];
+#pragma unroll
+                    for (int w = 0; w < 3; ++w) v += red[(w * NACC + (mb * (NBE + 1) + nb) * 4 + r) * 64 + lane];
+                    const int n = (nb < NBE ? nb * 16 : 0) + (lane & 15);
+                    if (nb < NBE) {
+                        if (n < NB * 9) a.partE[((size_t)sp * HALF + co) * (NB * 9) + n] = v;
+                        else if (n == NB * 9) a.bpartE[(size_t)sp * HALF + co] = v;
+                    } else {
+                        if (n < 9) a.partI[((size_t)sp * HALF + co) * 9 + n] = v;
+                        else if (n == 9) a.bpartI[(size_t)sp * HALF + co] = v;
+                    }
+                }
+            }
+    }
+}
+
 // up = interpolate(x, 2x, bilinear, align_corners=False) materialised, NHWC (B,h,w,C) ->
 // (B,2h,2w,C), the operation order of the forward's STAGE_UP gather (base_layers.py:198), so
 // the upsample conv's wgrad can run as a stride-1 wgrad on it
