@@ -79,11 +79,20 @@ def main():
     for _ in range(40):          # warm the clock
         _lib.check(L.cista_wgrad_ista_p(*args), "cista_wgrad_ista_p")
     torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(20):
+        L.cista_wgrad_ista_p(*args)
+    e1.record()
+    e1.synchronize()
+    launch_ms = e0.elapsed_time(e1) / 20
     L.cista_debug_set_wstamps(ctypes.c_void_p(buf.data_ptr()))
     _lib.check(L.cista_wgrad_ista_p(*args), "cista_wgrad_ista_p")
     torch.cuda.synchronize()
     L.cista_debug_set_wstamps(ctypes.c_void_p(0))
-    print(json.dumps(analyse(buf.cpu().numpy())), flush=True)
+    out = analyse(buf.cpu().numpy())
+    out["launch_ms_unstamped"] = round(launch_ms, 4)
+    print(json.dumps(out), flush=True)
 
 
 if __name__ == "__main__":

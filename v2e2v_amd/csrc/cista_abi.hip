@@ -1071,6 +1071,8 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     a.Cout = Cout; a.Cin = Cin;
     a.partial = k.ws.part;
     a.bpartial = db ? k.ws.bpart : nullptr;
+    a.off32 = (long long)a.B * Hout * Wout * Gc < (1LL << 31) &&
+              (long long)a.B * Hin * Win * (x0c > x1c ? x0c : x1c) < (1LL << 31);
     constexpr bool TR_S2 = XS == XS_S2 && CISTA_WGRAD_TR_S2;
     if (TR_S2 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 && Goff % 4 == 0 && x0c % 32 == 0 &&
         x1c % 32 == 0 && Hin == 2 * Hout && Win == 2 * Wout) {

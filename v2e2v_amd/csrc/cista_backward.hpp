@@ -273,6 +273,7 @@ struct WgradArgs {
     int vec4;                           // float4 staging: Gc, Goff, x0c, x1c, Cin % 4 == 0, NHWC
                                         // input, tile <= 16x16 (S1/UP) or 8x8 (S2)
     const float *gscale;                // wgrad_split_kernel: {s, 1/s} power-of-two scale of G
+    int off32;                          // G and X element offsets fit 31 bits (wgrad_tr fast path)
 };
 
 typedef float f32x4w __attribute__((ext_vector_type(4)));
@@ -751,6 +752,18 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
 // 8 x 18 input halo.  Stride 2 (W0): 2 x 16 output pixels (1 K-step) over a 5 x 33 input halo
 // whose columns are stored parity-split (the 17 even columns, then the 16 odd ones), so the
 // input columns 2x + dx - 1 of four consecutive output pixels are four consecutive LDS pixels.
+#ifndef CISTA_WT_IL
+#define CISTA_WT_IL 0     // 1: the next tile's loads interleaved with this tile's conversions
+#endif
+#ifndef CISTA_WT_FAST
+#define CISTA_WT_FAST 1   // 32-bit interior-tile loads in the staging waves (0: reflect / bounds per item)
+#endif
+#ifndef CISTA_WT_SGB
+#define CISTA_WT_SGB 0    // 1: sched_group_barrier order per MFMA step (reads, then MFMAs)
+#endif
+#ifndef CISTA_WT_PRIO
+#define CISTA_WT_PRIO 1   // staging waves at s_setprio 1 (the MFMA waves wait less at the tile barrier: 0.2165 -> 0.2137 ms)
+#endif
 template <int XS> struct WtGeo {
     static constexpr int S = XS == XS_S2 ? 2 : 1;
     static constexpr int TH = S == 2 ? 2 : 6;           // output rows per tile (x 16 columns)
@@ -855,20 +868,63 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         const int hp = 4 * (lw + 4 * u) + sp;                            // 0..HP-1 (+ masked)
         const int hy = hp / GE::HW, hx = hp - hy * GE::HW;
         if (GE::HP % 16 && hp >= GE::HP) return make_float4(0.f, 0.f, 0.f, 0.f);
+#ifdef CISTA_EXP_WT_NOLOAD
+        return make_float4((float)hy, (float)hx, (float)b, 1.0f);   // timing experiment: no X fetch
+#endif
         return wg_load_x4<XS>(a, b, GE::S * oy0 - 1 + hy, GE::S * ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
     };
+    auto load_g = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
+        const int p = 4 * (lw + 4 * u) + sp;                             // 0..NPX-1
+        const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+#ifdef CISTA_EXP_WT_NOLOAD
+        return make_float4((float)oy, (float)ox, 1.0f, 2.0f);           // timing experiment: no G fetch
+#endif
+        return (oy < a.Hout && ox < a.Wout)
+                   ? *reinterpret_cast<const float4 *>(a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff +
+                                                       co0 + 16 * sb + 4 * sq)
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+#if CISTA_WT_FAST
+    // fast path: a tile whose input halo lies inside the image and whose G pixels all exist loads
+    // from one 32-bit base offset per tile plus per-item constants (no reflection, no bounds, no
+    // 64-bit index math; those cost the staging waves' issue slots on the MFMA waves' SIMDs)
+    const int cix = ci0 + 16 * sb + 4 * sq;
+    const bool xs0 = cix < a.x0c;
+    const float *xseg = xs0 ? a.X0 : a.X1;
+    const int xsegC = xs0 ? a.x0c : a.x1c, xcc = xs0 ? cix : cix - a.x0c;
+    const bool xlane = cix < a.Cin && xseg != nullptr;
+    int xrel[GE::UX], grel[GE::UG];
+#pragma unroll
+    for (int u = 0; u < GE::UX; ++u) {
+        const int hp = 4 * (lw + 4 * u) + sp, hy = hp / GE::HW, hx = hp - hy * GE::HW;
+        xrel[u] = (GE::HP % 16 && hp >= GE::HP) ? -1 : (hy * a.Win + hx) * xsegC;
+    }
+#pragma unroll
+    for (int u = 0; u < GE::UG; ++u) {
+        const int p = 4 * (lw + 4 * u) + sp;
+        grel[u] = ((p >> 4) * a.Wout + (p & 15)) * a.Gc;
+    }
+#endif
     auto load_tile = [&](int tile) __attribute__((always_inline)) {
         int b, oy0, ox0;
         tile_origin(tile, b, oy0, ox0);
+#if CISTA_WT_FAST && !defined(CISTA_EXP_WT_NOLOAD)
+        const int iy0 = GE::S * oy0 - 1, ix0 = GE::S * ox0 - 1;
+        if (a.off32 && iy0 >= 0 && iy0 + GE::HR <= a.Hin && ix0 >= 0 && ix0 + GE::HW <= a.Win &&
+            oy0 + GE::TH <= a.Hout && ox0 + 16 <= a.Wout) {
+            const float *gb = a.G + (unsigned)(((b * a.Hout + oy0) * a.Wout + ox0) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
 #pragma unroll
-        for (int u = 0; u < GE::UG; ++u) {
-            const int p = 4 * (lw + 4 * u) + sp;                         // 0..NPX-1
-            const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
-            gv[u] = make_float4(0.f, 0.f, 0.f, 0.f);
-            if (oy < a.Hout && ox < a.Wout)
-                gv[u] = *reinterpret_cast<const float4 *>(
-                    a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
+            for (int u = 0; u < GE::UG; ++u) gv[u] = *reinterpret_cast<const float4 *>(gb + grel[u]);
+            const float *xb = xlane ? xseg + (unsigned)(((b * a.Hin + iy0) * a.Win + ix0) * xsegC + xcc) : a.G;
+#pragma unroll
+            for (int u = 0; u < GE::UX; ++u)
+                xv[u] = (xlane && xrel[u] >= 0) ? *reinterpret_cast<const float4 *>(xb + xrel[u])
+                                                : make_float4(0.f, 0.f, 0.f, 0.f);
+            return;
         }
+#endif
+#pragma unroll
+        for (int u = 0; u < GE::UG; ++u) gv[u] = load_g(b, oy0, ox0, u);
 #pragma unroll
         for (int u = 0; u < GE::UX; ++u) xv[u] = load_x(b, oy0, ox0, u);
     };
@@ -883,8 +939,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + pos * 16 + 4 * sq) = lo;
     };
     // registers -> LDS buffer (hi / lo planes); publishes whether this wave's X overflowed
-    auto commit = [&](_Float16 *buf, int *flag) __attribute__((always_inline)) {
+    // next >= 0: each item's register is refilled with tile `next`'s item right after it is
+    // stored, so the next tile's loads issue spread over the conversions (CISTA_WT_IL)
+    auto commit = [&](_Float16 *buf, int *flag, int next = -1) __attribute__((always_inline)) {
         _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
+        int nb_ = 0, noy = 0, nox = 0;
+        if (next >= 0) tile_origin(next, nb_, noy, nox);
 #pragma unroll
         for (int u = 0; u < GE::UG; ++u) {
             const int p = 4 * (lw + 4 * u) + sp;
@@ -894,12 +954,14 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
             split4(v, hi, lo);
             *reinterpret_cast<uint2 *>(Gp + sb * WT_GPL + p * 16 + 4 * sq) = hi;
             *reinterpret_cast<uint2 *>(Gp + (4 + sb) * WT_GPL + p * 16 + 4 * sq) = lo;
+            if (next >= 0) gv[u] = load_g(nb_, noy, nox, u);
         }
         float m = 0.0f;
 #pragma unroll
         for (int u = 0; u < GE::UX; ++u) {
             m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
             put_x(Xp, u, xv[u]);
+            if (next >= 0) xv[u] = load_x(nb_, noy, nox, u);
         }
         const bool ovf = m * sx >= 32768.0f && m < 3.0e38f;               // hi part would overflow
         const bool any = __ballot(ovf ? 1 : 0) != 0;
@@ -933,6 +995,10 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     if (loader) {
         // the roles run separate loops with the same barrier sequence, so the loaders' staging
         // registers and the MFMA waves' accumulators are never live at the same time
+#if CISTA_WT_PRIO
+        // the staging waves (the younger half) win VALU issue arbitration against the MFMA waves
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+#endif
         WT_STAMP(0, __builtin_amdgcn_s_memtime());
         if ((int)blockIdx.y < ntiles) {
             load_tile(blockIdx.y);
@@ -963,12 +1029,21 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 for (int u = 0; u < GE::UX; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
                 __syncthreads();
             }
+#ifdef CISTA_EXP_WT_IDLE
+            if (tile < 0)   // timing experiment: staging waves idle after the first tile (barriers only)
+#endif
             if (tile + a.nsplit < ntiles) {
                 // the other buffer was last read before the barrier that opened this iteration
+#if CISTA_WT_IL
+                commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1), tile + 2 * a.nsplit < ntiles ? tile + 2 * a.nsplit : -1);
+                WT_STAMP(3 + 3 * it, __builtin_amdgcn_s_memtime());
+                WT_STAMP(4 + 3 * it, __builtin_amdgcn_s_memtime());
+#else
                 commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1));
                 WT_STAMP(3 + 3 * it, __builtin_amdgcn_s_memtime());
                 if (tile + 2 * a.nsplit < ntiles) load_tile(tile + 2 * a.nsplit);
                 WT_STAMP(4 + 3 * it, __builtin_amdgcn_s_memtime());
+#endif
             }
             __syncthreads();
             WT_STAMP(5 + 3 * it, __builtin_amdgcn_s_memtime());
@@ -1043,6 +1118,16 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                     acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh[gb][u], xl[xb][v], acc[u][v][t], 0, 0, 0);
                     acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl[gb][u], xh[xb][v], acc[u][v][t], 0, 0, 0);
                 }
+#if CISTA_WT_SGB
+            // the next step's fragment reads first, then this step's 12 MFMAs: a read gets the
+            // whole step (12 x 16 cycles) to land (left alone, the scheduler sinks the reads below
+            // most of the MFMAs and the next step waits on them)
+            if (n + 1 < 9 * GE::KS) {
+                if (t == 8) __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
+                else __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
+            }
+            __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
+#endif
             __builtin_amdgcn_sched_barrier(0);
         }
         if (it < 120) WT_STAMP(2 + 2 * it, __builtin_amdgcn_s_memtime());
