@@ -1074,7 +1074,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     a.off32 = (long long)a.B * Hout * Wout * Gc < (1LL << 31) &&
               (long long)a.B * Hin * Win * (x0c > x1c ? x0c : x1c) < (1LL << 31);
     constexpr bool TR_S2 = XS == XS_S2 && CISTA_WGRAD_TR_S2;
-    if (TR_S2 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 && Goff % 4 == 0 && x0c % 32 == 0 &&
+    if (TR_S2 && a.off32 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 && Goff % 4 == 0 && x0c % 32 == 0 &&
         x1c % 32 == 0 && Hin == 2 * Hout && Win == 2 * Wout) {
         // W0 (stride 2): the split-f16 wgrad on 2 x 16-pixel tiles over a parity-split halo
         if constexpr (TR_S2) {
@@ -1093,7 +1093,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
             if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S2>)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S2>, dim3(nblk, ns), dim3(512), GE::LDS, k.wst, a);
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S2>, dim3(nblk, ns), dim3(WT_THREADS), GE::LDS, k.wst, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }
@@ -1105,7 +1105,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.tiles_y = (Hout + WS_TH - 1) / WS_TH;
         a.tiles_x = (Wout + WS_TW - 1) / WS_TW;
         const int ntiles = a.B * a.tiles_y * a.tiles_x;
-        if (CISTA_WGRAD_TR) {
+        if (CISTA_WGRAD_TR && a.off32) {
             static_assert(WtGeo<XS_S1>::TH == WS_TH && WS_TW == 16, "wgrad_tr_kernel tiles");
             // 64 x 64 blocks, one 8-wave workgroup per CU: splits fill the CUs once (and fit
             // the partial buffer: ns x Cout x Cin x 9 <= WG_BLOCKS x 32 x 32 x 9)
@@ -1118,7 +1118,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
             if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S1>)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S1>, dim3(nblk, ns), dim3(512), WtGeo<XS_S1>::LDS, k.wst, a);
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S1>, dim3(nblk, ns), dim3(WT_THREADS), WtGeo<XS_S1>::LDS, k.wst, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }

@@ -752,17 +752,16 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
 // 8 x 18 input halo.  Stride 2 (W0): 2 x 16 output pixels (1 K-step) over a 5 x 33 input halo
 // whose columns are stored parity-split (the 17 even columns, then the 16 odd ones), so the
 // input columns 2x + dx - 1 of four consecutive output pixels are four consecutive LDS pixels.
-#ifndef CISTA_WT_IL
-#define CISTA_WT_IL 0     // 1: the next tile's loads interleaved with this tile's conversions
+#ifndef CISTA_WT_MW
+#define CISTA_WT_MW 4     // MFMA waves per workgroup: 4 (32 co x 32 ci each) or 8 (32 co x 16 ci, 3 waves per SIMD; measured slower)
 #endif
-#ifndef CISTA_WT_FAST
-#define CISTA_WT_FAST 1   // 32-bit interior-tile loads in the staging waves (0: reflect / bounds per item)
-#endif
-#ifndef CISTA_WT_SGB
-#define CISTA_WT_SGB 0    // 1: sched_group_barrier order per MFMA step (reads, then MFMAs)
+constexpr int WT_NMW = CISTA_WT_MW, WT_THREADS = (CISTA_WT_MW + 4) * 64;
+static_assert(WT_NMW == 4 || WT_NMW == 8, "wgrad_tr MFMA waves");
+#ifndef CISTA_WT_XD
+#define CISTA_WT_XD 1     // MFMA-wave fragment reads this many steps ahead (1 or 2; 2 measured slower)
 #endif
 #ifndef CISTA_WT_PRIO
-#define CISTA_WT_PRIO 1   // staging waves at s_setprio 1 (the MFMA waves wait less at the tile barrier: 0.2165 -> 0.2137 ms)
+#define CISTA_WT_PRIO 1   // staging waves at s_setprio 1 (training 1727-1743 -> 1744-1745 frames/s same-box)
 #endif
 template <int XS> struct WtGeo {
     static constexpr int S = XS == XS_S2 ? 2 : 1;
@@ -826,15 +825,15 @@ __device__ unsigned long long *g_cista_wstamps;
 #define WT_STAMP(slot, v)                                                                           \
     do {                                                                                            \
         unsigned long long *_p = g_cista_wstamps;                                                   \
-        if (_p && lane == 0 && (wave & 3) == 0 && (slot) < 256)                                     \
-            _p[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 512 + (wave >> 2) * 256 + (slot)] = (v); \
+        if (_p && lane == 0 && (wave == 0 || wave == WT_NMW) && (slot) < 256)                       \
+            _p[((size_t)blockIdx.y * gridDim.x + blockIdx.x) * 512 + (wave >= WT_NMW) * 256 + (slot)] = (v); \
     } while (0)
 #else
 #define WT_STAMP(slot, v) do { } while (0)
 #endif
 
 template <int XS>
-__global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
+__global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs a) {
     using GE = WtGeo<XS>;
     constexpr int WT_GPL = GE::GPL, WT_XPL = GE::XPL, WT_BUF = GE::BUF;
     extern __shared__ u32x4 wsm4[];
@@ -844,13 +843,13 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ncb = (a.Cin + 63) / 64;
     const int co0 = (blockIdx.x / ncb) * 64, ci0 = (blockIdx.x % ncb) * 64;
-    const bool loader = wave >= 4;             // waves 0-3: MFMAs; waves 4-7: staging
+    const bool loader = wave >= WT_NMW;        // waves 0 .. NMW-1: MFMAs; the last 4: staging
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
     const float gsc = a.gscale[0];
     float sx = 1.0f;                           // X pre-scale in force (power of two, <= 1)
 
     // ---- staging (loader waves): item (pixel 4 set + sp, channel quad sq of plane sb) ----
-    const int lw = wave - 4;
+    const int lw = wave - WT_NMW;
     const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
     const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -864,65 +863,32 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         oy0 = ty * GE::TH;
         ox0 = tx * 16;
     };
-    auto load_x = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
-        const int hp = 4 * (lw + 4 * u) + sp;                            // 0..HP-1 (+ masked)
-        const int hy = hp / GE::HW, hx = hp - hy * GE::HW;
-        if (GE::HP % 16 && hp >= GE::HP) return make_float4(0.f, 0.f, 0.f, 0.f);
-#ifdef CISTA_EXP_WT_NOLOAD
-        return make_float4((float)hy, (float)hx, (float)b, 1.0f);   // timing experiment: no X fetch
-#endif
-        return wg_load_x4<XS>(a, b, GE::S * oy0 - 1 + hy, GE::S * ox0 - 1 + hx, ci0 + 16 * sb + 4 * sq);
-    };
-    auto load_g = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
-        const int p = 4 * (lw + 4 * u) + sp;                             // 0..NPX-1
-        const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
-#ifdef CISTA_EXP_WT_NOLOAD
-        return make_float4((float)oy, (float)ox, 1.0f, 2.0f);           // timing experiment: no G fetch
-#endif
-        return (oy < a.Hout && ox < a.Wout)
-                   ? *reinterpret_cast<const float4 *>(a.G + (((size_t)b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff +
-                                                       co0 + 16 * sb + 4 * sq)
-                   : make_float4(0.f, 0.f, 0.f, 0.f);
-    };
-#if CISTA_WT_FAST
-    // fast path: a tile whose input halo lies inside the image and whose G pixels all exist loads
-    // from one 32-bit base offset per tile plus per-item constants (no reflection, no bounds, no
-    // 64-bit index math; those cost the staging waves' issue slots on the MFMA waves' SIMDs)
+    // the lane's X channel quad: segment, its channel count and offset (the host launches this
+    // kernel only when every G and X element offset fits 31 bits: 32-bit index math throughout)
     const int cix = ci0 + 16 * sb + 4 * sq;
     const bool xs0 = cix < a.x0c;
     const float *xseg = xs0 ? a.X0 : a.X1;
     const int xsegC = xs0 ? a.x0c : a.x1c, xcc = xs0 ? cix : cix - a.x0c;
     const bool xlane = cix < a.Cin && xseg != nullptr;
-    int xrel[GE::UX], grel[GE::UG];
-#pragma unroll
-    for (int u = 0; u < GE::UX; ++u) {
-        const int hp = 4 * (lw + 4 * u) + sp, hy = hp / GE::HW, hx = hp - hy * GE::HW;
-        xrel[u] = (GE::HP % 16 && hp >= GE::HP) ? -1 : (hy * a.Win + hx) * xsegC;
-    }
-#pragma unroll
-    for (int u = 0; u < GE::UG; ++u) {
-        const int p = 4 * (lw + 4 * u) + sp;
-        grel[u] = ((p >> 4) * a.Wout + (p & 15)) * a.Gc;
-    }
-#endif
+    auto load_x = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
+        const int hp = 4 * (lw + 4 * u) + sp;                            // 0..HP-1 (+ masked)
+        const int hy = hp / GE::HW, hx = hp - hy * GE::HW;
+        if (GE::HP % 16 && hp >= GE::HP) return make_float4(0.f, 0.f, 0.f, 0.f);
+        const int y = reflect_clamp(GE::S * oy0 - 1 + hy, a.Hin), x = reflect_clamp(GE::S * ox0 - 1 + hx, a.Win);
+        return xlane ? *reinterpret_cast<const float4 *>(xseg + (unsigned)(((b * a.Hin + y) * a.Win + x) * xsegC + xcc))
+                     : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
+    auto load_g = [&](int b, int oy0, int ox0, int u) __attribute__((always_inline)) {
+        const int p = 4 * (lw + 4 * u) + sp;                             // 0..NPX-1
+        const int oy = oy0 + (p >> 4), ox = ox0 + (p & 15);
+        return (oy < a.Hout && ox < a.Wout)
+                   ? *reinterpret_cast<const float4 *>(a.G + (unsigned)(((b * a.Hout + oy) * a.Wout + ox) * a.Gc + a.Goff +
+                                                                        co0 + 16 * sb + 4 * sq))
+                   : make_float4(0.f, 0.f, 0.f, 0.f);
+    };
     auto load_tile = [&](int tile) __attribute__((always_inline)) {
         int b, oy0, ox0;
         tile_origin(tile, b, oy0, ox0);
-#if CISTA_WT_FAST && !defined(CISTA_EXP_WT_NOLOAD)
-        const int iy0 = GE::S * oy0 - 1, ix0 = GE::S * ox0 - 1;
-        if (a.off32 && iy0 >= 0 && iy0 + GE::HR <= a.Hin && ix0 >= 0 && ix0 + GE::HW <= a.Win &&
-            oy0 + GE::TH <= a.Hout && ox0 + 16 <= a.Wout) {
-            const float *gb = a.G + (unsigned)(((b * a.Hout + oy0) * a.Wout + ox0) * a.Gc + a.Goff + co0 + 16 * sb + 4 * sq);
-#pragma unroll
-            for (int u = 0; u < GE::UG; ++u) gv[u] = *reinterpret_cast<const float4 *>(gb + grel[u]);
-            const float *xb = xlane ? xseg + (unsigned)(((b * a.Hin + iy0) * a.Win + ix0) * xsegC + xcc) : a.G;
-#pragma unroll
-            for (int u = 0; u < GE::UX; ++u)
-                xv[u] = (xlane && xrel[u] >= 0) ? *reinterpret_cast<const float4 *>(xb + xrel[u])
-                                                : make_float4(0.f, 0.f, 0.f, 0.f);
-            return;
-        }
-#endif
 #pragma unroll
         for (int u = 0; u < GE::UG; ++u) gv[u] = load_g(b, oy0, ox0, u);
 #pragma unroll
@@ -939,12 +905,8 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         *reinterpret_cast<uint2 *>(Xp + (4 + sb) * WT_XPL + pos * 16 + 4 * sq) = lo;
     };
     // registers -> LDS buffer (hi / lo planes); publishes whether this wave's X overflowed
-    // next >= 0: each item's register is refilled with tile `next`'s item right after it is
-    // stored, so the next tile's loads issue spread over the conversions (CISTA_WT_IL)
-    auto commit = [&](_Float16 *buf, int *flag, int next = -1) __attribute__((always_inline)) {
+    auto commit = [&](_Float16 *buf, int *flag) __attribute__((always_inline)) {
         _Float16 *Gp = buf, *Xp = buf + 8 * WT_GPL;
-        int nb_ = 0, noy = 0, nox = 0;
-        if (next >= 0) tile_origin(next, nb_, noy, nox);
 #pragma unroll
         for (int u = 0; u < GE::UG; ++u) {
             const int p = 4 * (lw + 4 * u) + sp;
@@ -954,14 +916,12 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
             split4(v, hi, lo);
             *reinterpret_cast<uint2 *>(Gp + sb * WT_GPL + p * 16 + 4 * sq) = hi;
             *reinterpret_cast<uint2 *>(Gp + (4 + sb) * WT_GPL + p * 16 + 4 * sq) = lo;
-            if (next >= 0) gv[u] = load_g(nb_, noy, nox, u);
         }
         float m = 0.0f;
 #pragma unroll
         for (int u = 0; u < GE::UX; ++u) {
             m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
             put_x(Xp, u, xv[u]);
-            if (next >= 0) xv[u] = load_x(nb_, noy, nox, u);
         }
         const bool ovf = m * sx >= 32768.0f && m < 3.0e38f;               // hi part would overflow
         const bool any = __ballot(ovf ? 1 : 0) != 0;
@@ -980,11 +940,11 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         sx = st;
         return r;
     };
-    auto acc_zero = [](f32x4 (&acc)[2][2][9]) __attribute__((always_inline)) {
+    auto acc_zero = [](auto &acc) __attribute__((always_inline)) {
 #pragma unroll
         for (int u = 0; u < 2; ++u)
 #pragma unroll
-            for (int v = 0; v < 2; ++v)
+            for (int v = 0; v < (int)(sizeof(acc[0]) / sizeof(acc[0][0])); ++v)
 #pragma unroll
                 for (int t = 0; t < 9; ++t) acc[u][v][t] = f32x4{0.f, 0.f, 0.f, 0.f};
     };
@@ -997,7 +957,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
         // registers and the MFMA waves' accumulators are never live at the same time
 #if CISTA_WT_PRIO
         // the staging waves (the younger half) win VALU issue arbitration against the MFMA waves
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 256) __builtin_amdgcn_s_setprio(1);
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WT_NMW) __builtin_amdgcn_s_setprio(1);
 #endif
         WT_STAMP(0, __builtin_amdgcn_s_memtime());
         if ((int)blockIdx.y < ntiles) {
@@ -1029,36 +989,28 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 for (int u = 0; u < GE::UX; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
                 __syncthreads();
             }
-#ifdef CISTA_EXP_WT_IDLE
-            if (tile < 0)   // timing experiment: staging waves idle after the first tile (barriers only)
-#endif
             if (tile + a.nsplit < ntiles) {
                 // the other buffer was last read before the barrier that opened this iteration
-#if CISTA_WT_IL
-                commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1), tile + 2 * a.nsplit < ntiles ? tile + 2 * a.nsplit : -1);
-                WT_STAMP(3 + 3 * it, __builtin_amdgcn_s_memtime());
-                WT_STAMP(4 + 3 * it, __builtin_amdgcn_s_memtime());
-#else
                 commit(sm + (bi ^ 1) * WT_BUF, xfl + 4 * (bi ^ 1));
                 WT_STAMP(3 + 3 * it, __builtin_amdgcn_s_memtime());
                 if (tile + 2 * a.nsplit < ntiles) load_tile(tile + 2 * a.nsplit);
                 WT_STAMP(4 + 3 * it, __builtin_amdgcn_s_memtime());
-#endif
             }
             __syncthreads();
             WT_STAMP(5 + 3 * it, __builtin_amdgcn_s_memtime());
         }
         if (do_bias) {
-            reinterpret_cast<float4 *>(wsm4)[tid - 256] = bsum;
+            reinterpret_cast<float4 *>(wsm4)[tid - 64 * WT_NMW] = bsum;
             __syncthreads();
         }
         return;
     }
 
-    // ---- MFMA waves: 32 co (planes pco, pco + 1) x 32 ci (planes pci, pci + 1) ----
-    const int pco = 2 * (wave >> 1), pci = 2 * (wave & 1);
+    // ---- MFMA waves: 32 co (planes pco, pco + 1) x NV x 16 ci (planes pci .. pci + NV - 1) ----
+    constexpr int NV = WT_NMW == 8 ? 1 : 2, WPC = 4 / NV;          // ci planes per wave, waves per co pair
+    const int pco = 2 * (wave / WPC), pci = NV * (wave % WPC);
     const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
-    f32x4 acc[2][2][9];
+    f32x4 acc[2][NV][9];
     acc_zero(acc);
     WT_STAMP(0, __builtin_amdgcn_s_memtime());
     WT_STAMP(252, __builtin_amdgcn_s_memrealtime());
@@ -1074,7 +1026,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int v = 0; v < 2; ++v)
+                for (int v = 0; v < NV; ++v)
 #pragma unroll
                     for (int t = 0; t < 9; ++t) acc[u][v][t] *= r;
             __syncthreads();
@@ -1090,44 +1042,37 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
                 gl[u] = cat_frag(tr_read(Gp, off + 4 * WT_GPL), tr_read(Gp, off + 4 * WT_GPL + 256));
             }
         };
-        auto read_x = [&](int s, int t, f16x8 (&xh)[2], f16x8 (&xl)[2]) __attribute__((always_inline)) {
+        auto read_x = [&](int s, int t, f16x8 (&xh)[NV], f16x8 (&xl)[NV]) __attribute__((always_inline)) {
             const int dy = t / 3, dx = t % 3;
             constexpr int R1 = GE::S * GE::HW * 16;     // K row 1 (the next output row) in halves
 #pragma unroll
-            for (int v = 0; v < 2; ++v) {
+            for (int v = 0; v < NV; ++v) {
                 const int off = (pci + v) * WT_XPL + GE::kpos(s, 0, dy, dx, 4 * kg + rq) * 16 + 4 * rp;
                 xh[v] = cat_frag(tr_read(Xp, off), tr_read(Xp, off + R1));
                 xl[v] = cat_frag(tr_read(Xp, off + 4 * WT_XPL), tr_read(Xp, off + 4 * WT_XPL + R1));
             }
         };
-        f16x8 gh[2][2], gl[2][2], xh[2][2], xl[2][2];
+        // XD = 1: fragments read one step ahead (double buffer); 2: two steps ahead (X triple
+        // buffer, the next K-step's G two taps early), so a read has a whole step (12 MFMAs)
+        // between its issue and the step that uses it even where the scheduler sinks it
+        constexpr int XD = CISTA_WT_XD, NXB = XD + 1, NSTEP = 9 * GE::KS;
+        f16x8 gh[2][2], gl[2][2], xh[NXB][NV], xl[NXB][NV];
         read_g(0, gh[0], gl[0]);
-        read_x(0, 0, xh[0], xl[0]);
 #pragma unroll
-        for (int n = 0; n < 9 * GE::KS; ++n) {
-            const int s = n / 9, t = n % 9, xb = n & 1, gb = s & 1;
-            if (n + 1 < 9 * GE::KS) {
-                read_x((n + 1) / 9, (n + 1) % 9, xh[xb ^ 1], xl[xb ^ 1]);
-                if (t == 8) read_g(s + 1, gh[gb ^ 1], gl[gb ^ 1]);
-            }
+        for (int d = 0; d < XD; ++d) read_x(d / 9, d % 9, xh[d], xl[d]);
+#pragma unroll
+        for (int n = 0; n < NSTEP; ++n) {
+            const int s = n / 9, t = n % 9, xb = n % NXB, gb = s & 1;
+            if (n + XD < NSTEP) read_x((n + XD) / 9, (n + XD) % 9, xh[(n + XD) % NXB], xl[(n + XD) % NXB]);
+            if (s + 1 < GE::KS && t == 9 - XD) read_g(s + 1, gh[gb ^ 1], gl[gb ^ 1]);
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
-                for (int v = 0; v < 2; ++v) {
+                for (int v = 0; v < NV; ++v) {
                     acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh[gb][u], xh[xb][v], acc[u][v][t], 0, 0, 0);
                     acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gh[gb][u], xl[xb][v], acc[u][v][t], 0, 0, 0);
                     acc[u][v][t] = __builtin_amdgcn_mfma_f32_16x16x32_f16(gl[gb][u], xh[xb][v], acc[u][v][t], 0, 0, 0);
                 }
-#if CISTA_WT_SGB
-            // the next step's fragment reads first, then this step's 12 MFMAs: a read gets the
-            // whole step (12 x 16 cycles) to land (left alone, the scheduler sinks the reads below
-            // most of the MFMAs and the next step waits on them)
-            if (n + 1 < 9 * GE::KS) {
-                if (t == 8) __builtin_amdgcn_sched_group_barrier(0x100, 16, 0);
-                else __builtin_amdgcn_sched_group_barrier(0x100, 8, 0);
-            }
-            __builtin_amdgcn_sched_group_barrier(0x008, 12, 0);
-#endif
             __builtin_amdgcn_sched_barrier(0);
         }
         if (it < 120) WT_STAMP(2 + 2 * it, __builtin_amdgcn_s_memtime());
@@ -1151,7 +1096,7 @@ __global__ __launch_bounds__(512, 1) void wgrad_tr_kernel(const WgradArgs a) {
     const float inv = a.gscale[1] * (1.0f / sx);
     float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
 #pragma unroll
-    for (int v = 0; v < 2; ++v) {
+    for (int v = 0; v < NV; ++v) {
         const int ci = ci0 + 16 * (pci + v) + (lane & 15);
         if (ci >= a.Cin) continue;
 #pragma unroll
