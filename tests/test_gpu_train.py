@@ -305,8 +305,9 @@ def test_wgrad_tr_s2_kernel_matches_fp64(xscale):
     assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
 
 
-@pytest.mark.parametrize("H,W,C", [(6, 8, 32), (8, 12, 32), (12, 10, 32), (12, 16, 96), (10, 14, 128), (8, 8, 256)])
-def test_small_images_bptt_against_fp64_autograd(H, W, C):
+@pytest.mark.parametrize("H,W,C,NB", [(6, 8, 32, 5), (8, 12, 32, 5), (12, 10, 32, 5), (12, 16, 96, 5), (10, 14, 128, 5),
+                                      (8, 8, 256, 5), (16, 20, 64, 1), (12, 16, 32, 8), (14, 18, 64, 3)])
+def test_small_images_bptt_against_fp64_autograd(H, W, C, NB):
     """The dgrads fold the reflect padding in their epilogue (EPI_FOLD + fold_fix_kernel) when the
     half-resolution input has rows 1 and n-2 distinct (h, w >= 4) and take the padded-domain
     dgrad + fold_reflect_kernel pass otherwise: 6x8 (h = 3, the pass), 8x12 (h = 4, the smallest
@@ -316,13 +317,13 @@ def test_small_images_bptt_against_fp64_autograd(H, W, C):
     training path beyond the reference default's channel counts (any multiple of 32)."""
     from oracle.cista_oracle_torch import CistaLSTCTorchCPU
     depth, B = 2, 2
-    params = fx.stress_params(C, depth, 5, seed=H * 100 + W, lam=0.05)
-    m = CistaLSTCNet([H, W], base_channels=C, depth=depth, num_bins=5)
+    params = fx.stress_params(C, depth, NB, seed=H * 100 + W, lam=0.05)
+    m = CistaLSTCNet([H, W], base_channels=C, depth=depth, num_bins=NB)
     sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, depth)
     m.load_state_dict(sd, strict=True)
     m = m.to(DEV)
     rng = np.random.default_rng(H * W)
-    vox = rng.standard_normal((2, B, 5, H, W)).astype(np.float32)
+    vox = rng.standard_normal((2, B, NB, H, W)).astype(np.float32)
     target = rng.random((B, 1, H, W)).astype(np.float32)
     prev, state = torch.zeros(B, 1, H, W, device=DEV), None
     for f in range(2):
