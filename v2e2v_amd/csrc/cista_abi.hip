@@ -46,6 +46,7 @@ struct Layout {
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
     size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS, wU4, bU4, wUT, bU;
     size_t w4p, b4p;                       // W0 dgrad as a four-phase conv (pack_w0phase_kernel)
+    size_t wsp;                            // weight |max| partials of the pack (weight_absmax_kernel)
     size_t total;
 };
 
@@ -85,6 +86,7 @@ Layout make_layout(const cista_config &cfg) {
     L.bU = off; off = align_up(off + (size_t)C * 4);
     L.w4p = off; off = align_up(off + (size_t)(C / 32) * 9 * (4 * C / 16) * 2 * 64 * 16);
     L.b4p = off; off = align_up(off + (size_t)4 * C * 4);
+    L.wsp = off; off = align_up(off + (size_t)CV_COUNT * WS_PARTS * 4);
     L.total = off;
     return L;
 }
@@ -1607,13 +1609,26 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
     const float *bs[CV_COUNT] = {p->W0_b, p->P0_b, p->gates_b, p->out_gates_b, p->D_b, p->P_b,
                                  p->Dg_b, p->lstm_b, p->up_b, blobw<float>(packed, L.bS),
                                  blobw<float>(packed, L.bU4)};
+    {   // every conv's weight scale pair: two launches (WeightScaleJobs)
+        static_assert(CV_COUNT <= WS_JOBS, "weight scale jobs");
+        WeightScaleJobs j;
+        memset(&j, 0, sizeof(j));
+        j.jobs = CV_COUNT;
+        j.part = blobw<float>(packed, L.wsp);
+        for (int i = 0; i < CV_COUNT; ++i) {
+            const ConvShape s = conv_shape(i, C);
+            j.w[i] = ws[i];
+            j.n[i] = (long)s.cout * s.cin * 9;
+            j.scale[i] = blobw<float>(packed, L.sc[i]);
+        }
+        hipLaunchKernelGGL(weight_absmax_kernel, dim3(WS_PARTS, CV_COUNT), dim3(256), 0, st, j);
+        hipLaunchKernelGGL(weight_scale_finalize_kernel, dim3(CV_COUNT), dim3(64), 0, st, j);
+    }
     for (int i = 0; i < CV_COUNT; ++i) {
         const ConvShape s = conv_shape(i, C);
         PackArgs a;
         a.w = ws[i]; a.b = bs[i];
         a.scale = blobw<float>(packed, L.sc[i]);
-        hipLaunchKernelGGL(weight_scale_kernel, dim3(1), dim3(1024), 0, st, ws[i],
-                           (long)s.cout * s.cin * 9, a.scale);
         a.wp = blobw<u32x4>(packed, L.wp[i]);
         a.bp = blobw<float>(packed, L.bp[i]);
         a.Cout = s.cout; a.Cin = s.cin; a.G = s.G;

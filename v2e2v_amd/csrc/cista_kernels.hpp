@@ -2241,7 +2241,7 @@ __global__ __launch_bounds__(64) void up_border_kernel(const UpBorderArgs a) {
 struct PackArgs {
     const float *w;      // [Cout][Cin][3][3]
     const float *b;      // [Cout]
-    float *scale;        // [2]: {pre-scale s, 1/s}, written by weight_scale_kernel
+    float *scale;        // [2]: {pre-scale s, 1/s}, written by weight_scale_finalize_kernel
     u32x4 *wp;           // [kc][tap][nt][part][lane]
     float *bp;           // [N] packed-column bias
     int Cout, Cin, G;    // G: gates grouped per channel block
@@ -2278,25 +2278,45 @@ __global__ void pack_conv_kernel(const PackArgs a) {
 
 // Per-layer power-of-two pre-scale: s = 2^floor(log2(16384 / max|w|)), clamped to 2^[-24, 40],
 // so w*s stays well inside fp16 range and its lo part stays a normal fp16 number.
-__global__ __launch_bounds__(1024) void weight_scale_kernel(const float *w, long n, float *scale) {
-    __shared__ float red[1024];
+// Every conv's weight |max| at once (was one single-workgroup kernel per conv: 11 serial launches
+// of up to 190 us per parameter pack, i.e. per training step): grid (WS_PARTS, jobs), each
+// workgroup's maximum to part[job][blockIdx.x]; weight_scale_finalize_kernel turns them into the
+// {s, 1/s} power-of-two pairs (s brings the |max| to [2^13, 2^14); a maximum is order-free)
+constexpr int WS_PARTS = 64, WS_JOBS = 16;
+struct WeightScaleJobs {
+    const float *w[WS_JOBS];
+    long n[WS_JOBS];
+    float *scale[WS_JOBS];
+    float *part;           // [jobs][WS_PARTS]
+    int jobs;
+};
+__global__ __launch_bounds__(256) void weight_absmax_kernel(const WeightScaleJobs j) {
+    __shared__ float red[256];
+    const int job = blockIdx.y;
+    const float *w = j.w[job];
+    const long n = j.n[job];
     float m = 0.0f;
-    for (long i = threadIdx.x; i < n; i += blockDim.x) m = fmaxf(m, fabsf(w[i]));
+    for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)WS_PARTS * 256) m = fmaxf(m, fabsf(w[i]));
     red[threadIdx.x] = m;
     __syncthreads();
-    for (int s = 512; s > 0; s >>= 1) {
+    for (int s = 128; s > 0; s >>= 1) {
         if ((int)threadIdx.x < s) red[threadIdx.x] = fmaxf(red[threadIdx.x], red[threadIdx.x + s]);
         __syncthreads();
     }
+    if (threadIdx.x == 0) j.part[job * WS_PARTS + blockIdx.x] = red[0];
+}
+__global__ __launch_bounds__(64) void weight_scale_finalize_kernel(const WeightScaleJobs j) {
+    const int job = blockIdx.x;
+    float m = threadIdx.x < WS_PARTS ? j.part[job * WS_PARTS + threadIdx.x] : 0.0f;
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
     if (threadIdx.x == 0) {
-        const float mx = red[0];
         int e = 0;
-        if (mx > 0.0f && isfinite(mx)) {
-            e = (int)floorf(log2f(16384.0f / mx));
+        if (m > 0.0f && isfinite(m)) {
+            e = (int)floorf(log2f(16384.0f / m));
             e = e < -24 ? -24 : (e > 40 ? 40 : e);
         }
-        scale[0] = ldexpf(1.0f, e);
-        scale[1] = ldexpf(1.0f, -e);
+        j.scale[job][0] = ldexpf(1.0f, e);
+        j.scale[job][1] = ldexpf(1.0f, -e);
     }
 }
 
