@@ -761,7 +761,7 @@ static_assert(WT_NMW == 4 || WT_NMW == 8, "wgrad_tr MFMA waves");
 #define CISTA_WT_XD 1     // MFMA-wave fragment reads this many steps ahead (1 or 2; 2 measured slower)
 #endif
 #ifndef CISTA_WT_PRIO
-#define CISTA_WT_PRIO 1   // staging waves at s_setprio 1 (training 1727-1743 -> 1744-1745 frames/s same-box)
+#define CISTA_WT_PRIO 1   // staging waves at s_setprio CISTA_WT_PRIO (1: training 1727-1743 -> 1744-1745 frames/s same-box)
 #endif
 template <int XS> struct WtGeo {
     static constexpr int S = XS == XS_S2 ? 2 : 1;
@@ -957,7 +957,7 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
         // registers and the MFMA waves' accumulators are never live at the same time
 #if CISTA_WT_PRIO
         // the staging waves (the younger half) win VALU issue arbitration against the MFMA waves
-        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WT_NMW) __builtin_amdgcn_s_setprio(1);
+        if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WT_NMW) __builtin_amdgcn_s_setprio(CISTA_WT_PRIO);
 #endif
         WT_STAMP(0, __builtin_amdgcn_s_memtime());
         if ((int)blockIdx.y < ntiles) {
