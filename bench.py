@@ -199,8 +199,7 @@ def v2e2v_main(args, torch, vd, rank, world, device):
                                                              for v in layers.values()), 4),
             "layers_ms": {k: round(v["ms"], 4) for k, v in layers.items()}}),
             flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    vd.finalize()
 
 
 class _NpRng:
@@ -271,7 +270,8 @@ def train_main(args, torch, vd, rank, world, device):
     he_init_(torch, model, seed=7)
     model = model.to(device).train()
     net = model
-    if world > 1:
+    if vd.active():
+        # under torchrun (any N, N=1 included): one bucketed RCCL all-reduce of the gradients
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index],
                                                         broadcast_buffers=False)
     opt = torch.optim.Adam(model.parameters(), lr=1e-4)
@@ -324,12 +324,12 @@ def train_main(args, torch, vd, rank, world, device):
             "data": "synthetic (GPU-generated 15000-event voxels, random targets; L1 + 1-SSIM loss)",
             "config": {"workload": f"train_e2v BPTT len {L}, batch {B}/GPU, {H}x{W}",
                        "batch_per_gpu": B, "global_batch": B * world, "len_sequence": L,
-                       "parallelism": f"ddp{world}" if world > 1 else "single"},
+                       "parallelism": f"ddp{world}" if vd.active() else "single",
+                       "process_group": (torch.distributed.get_backend() if vd.active() else None)},
             "loss": float(loss.item()),
             "roofline": roofline, "cpu_baseline": cpu,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    vd.finalize()
 
 
 def train_roofline(torch, model, lib_mod, B, H, W, device, reps=10):
@@ -855,8 +855,7 @@ def main():
             "batch_sweep": sweep,
         }
         print(json.dumps(out), flush=True)
-    if world > 1:
-        torch.distributed.destroy_process_group()
+    vd.finalize()
 
 
 if __name__ == "__main__":

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session: parity tests -> smoke -> bench (-> optional rocprof).  Every GPU step has
 # its own time limit; after a crash / fault / timeout nothing else touches the GPU.
-# usage: bash scripts/gpu_check.sh [tests] [smoke] [bench] [prof] [pmc]
+# usage: bash scripts/gpu_check.sh [tests] [smoke] [bench] [prof] [ttests] [tbench] [tprof] [vbench] [vprof] [pmc] ...
 mkdir -p gpurun_out
 ok() { local rc=$1; [ "$rc" -eq 0 ] || [ "$rc" -eq 1 ]; }   # 1 = test failures, not a crash
 for step in "$@"; do
@@ -36,12 +36,6 @@ for step in "$@"; do
       cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
       timeout -k 10 600 rocprofv3 --kernel-trace --stats -f csv -d gpurun_out/profv -o run -- python3 bench.py --mode v2e2v --steps 1 --warmup 1 > gpurun_out/profv_bench.json 2> gpurun_out/profv.err
       rc=$?; echo "vprof rc=$rc"; tail -3 gpurun_out/profv.err; [ $rc -eq 0 ] || exit $rc ;;
-    vtests)
-      # persistent-loop parity of every variant build (bit-exact batch vs single runs)
-      for f in v2e2v_amd/variants/*.so; do
-        CISTA_HIP_LIB=$f timeout -k 10 300 python -m pytest tests/test_gpu_parity.py -q -p no:cacheprovider -k "stage or f3 or oracle_random or f1_sequence or batch" > gpurun_out/vtests_$(basename $f .so).log 2>&1
-        rc=$?; echo "vtests $(basename $f) rc=$rc"; tail -1 gpurun_out/vtests_$(basename $f .so).log; ok $rc || exit $rc
-      done ;;
     ab)
       timeout -k 10 900 bash scripts/ab_layers.sh ${AB_B:-64}
       rc=$?; echo "ab rc=$rc"; cat gpurun_out/layers.jsonl; [ $rc -eq 0 ] || exit $rc ;;

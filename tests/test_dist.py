@@ -51,6 +51,41 @@ def test_gloo_sharding_and_reductions(world):
         assert sm == 37.0
 
 
+def _single_worker(port, q):
+    # torchrun --nproc-per-node 1 sets the rank environment at world size 1: the process group
+    # must still come up (the N=1 scaling point runs the same DDP all-reduce as N=8)
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    r, w, _ = vd.init("gloo")
+    up = vd.active()
+    m = torch.nn.Linear(3, 2)
+    net = torch.nn.parallel.DistributedDataParallel(m)
+    net(torch.ones(4, 3)).sum().backward()
+    g = m.weight.grad.clone()
+    vd.barrier()
+    vd.finalize()
+    q.put((r, w, up, vd.active(), g.tolist()))
+
+
+def test_world_size_one_under_launcher_initialises_process_group():
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_single_worker, args=(_free_port(), q))
+    p.start()
+    r, w, up, after, g = q.get(timeout=120)
+    p.join(timeout=60)
+    assert p.exitcode == 0
+    assert (r, w, up, after) == (0, 1, True, False)
+    assert g == [[4.0, 4.0, 4.0], [4.0, 4.0, 4.0]]      # DDP at world size 1: the all-reduce is exact
+
+
+def test_no_process_group_without_launcher(monkeypatch):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    assert not vd.under_launcher()
+    assert vd.init("gloo") == (0, 1, 0)
+    assert not vd.active()
+
+
 def test_shard_partition_properties():
     for n in (0, 1, 7, 64, 65):
         for w in (1, 2, 3, 8):

@@ -210,23 +210,7 @@ bool allow_big_lds(const void *kern) {
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
-// compute units of the current device (persistent launches size their grid by it)
-[[maybe_unused]] int device_cus() {
-    static std::mutex mu;
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 256;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!cus[dev]) {
-        int n = 0;
-        if (hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0) n = 256;
-        cus[dev] = n;
-    }
-    return cus[dev];
-}
-
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2,
-          bool PERS = false>
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
     constexpr int S = STAGE == STAGE_S2 ? 2 : 1;
@@ -248,14 +232,13 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
     // the training variant (SV) only for epilogues that save activations, and only when asked
     constexpr bool HAS_SV = EPI == EPI_ISTA_P || EPI == EPI_LSTC_CELL || EPI == EPI_LSTC_OUT || EPI == EPI_LSTM;
-    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false, OCC, PERS>;
+    auto kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, false, OCC>;
     if constexpr (HAS_SV)
         if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr)
-            kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC, PERS>;
+            kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
 #if CISTA_XCD
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
-    static_assert(!PERS || CISTA_XCD, "persistent items use the 1-D grid");
 #else
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
 #endif
@@ -269,22 +252,7 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
-#ifdef CISTA_EXP_ONEWG
-    // timing experiment: one workgroup per CU (LDS-limited), no overlap between workgroups
-    if (lds < 96 * 1024) lds = 96 * 1024;
-#endif
-    if constexpr (PERS) {
-        // one workgroup per resident slot walking the items (dma_chunk0); only where every slot
-        // gets more than one item, the epilogue's LDS fits in the first staging image (the raw
-        // image of the next item lands in the second) and the tile is not a border strip
-        const long items = (long)a.B * t.ty * t.tx * (a.N / nblk_cols);
-        const long slots = (long)device_cus() * (OCC * 4 / NWV);
-        if (items <= slots || t.lds / 2 < epi_lds + 12 * NWV || a.border != 0 || (slots & 7))
-            return launch_conv_cfg<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, OCC, false>(a, st);
-        a.items = (int)items;
-        grid = dim3((unsigned)slots);
-    }
+    const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
     hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
     return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
 }
@@ -303,23 +271,14 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #ifndef CISTA_PF_MT
 #define CISTA_PF_MT 12
 #endif
-#ifndef CISTA_S2DB
-#define CISTA_S2DB 0      // stride-2 W0: 0 single-buffered 128-px tiles; 1/2 double-buffered 64-px
-#endif
 #ifndef CISTA_SMALL_GRID
 #define CISTA_SMALL_GRID 1   // latency tiles for grids that would not fill the chip (small B)
-#endif
-#ifndef CISTA_ISTA8
-#define CISTA_ISTA8 0            // 1: ISTA D conv on 8-wave workgroups (measured 5 % slower), 2: also ISTA P (spills)
 #endif
 #ifndef CISTA_W0_PHASE
 #define CISTA_W0_PHASE 1         // W0's dgrad as a four-phase MFMA conv (0: the VALU dgrad_s2_kernel)
 #endif
 #ifndef CISTA_DGRAD_SMALL
 #define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
-#endif
-#ifndef CISTA_PERSIST
-#define CISTA_PERSIST 0   // forward stride-1 convs at large batch: persistent items, next tile's chunk 0 by LDS-DMA
 #endif
 #ifndef CISTA_WIDE
 #define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
@@ -338,13 +297,6 @@ inline bool small_grid(const ConvArgs &a, int wg_px, int wg_cols, int limit = 38
 template <int STAGE, int EPI, int G>
 int launch_conv(const ConvArgs &a, hipStream_t st) {
     if constexpr (STAGE == STAGE_S2) {
-#if CISTA_S2DB == 1
-        // double-buffered K loop: 64-pixel tiles keep two stride-2 halo images (17x17 px)
-        // within the 80 KiB LDS of two workgroups per CU
-        if (a.N % 64 == 0) return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 5>(a, st);
-#elif CISTA_S2DB == 2
-        if (a.N % 64 == 0) return launch_conv_cfg<1, 4, 4, 1, STAGE, EPI, G, true, 5>(a, st);
-#endif
         if (a.N % 64 == 0) return launch_conv_cfg<2, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N % 32 == 0) return launch_conv_cfg<2, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
@@ -375,20 +327,13 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
                 else return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
             }
         }
-        if constexpr (CISTA_ISTA8 && STAGE == STAGE_S1 && G == 1 && (EPI == EPI_ISTA_D || EPI == EPI_ISTA_P)) {
-            // 8-wave workgroups on the same 192-pixel tiles: 4 waves per SIMD at 2 workgroups
-            // per CU, so one workgroup's staging / epilogue HBM phases overlap more MFMA waves
-            if (a.N == 128 && CISTA_ISTA8 > 1) return launch_conv_cfg<6, 2, 2, 4, STAGE, EPI, G, true, 2, 4>(a, st);
-            if (a.N == 64) return launch_conv_cfg<3, 2, 4, 2, STAGE, EPI, G, true, 2, 4>(a, st);
-        }
-        constexpr bool PS = STAGE == STAGE_S1 && CISTA_PERSIST;   // (falls back per launch, launch_conv_cfg)
         if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
-            if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4, 2, PS>(a, st);
+            if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
         if constexpr (G == 4) {
             if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
         } else {
-            if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4, 2, PS>(a, st);
-            if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4, 2, PS>(a, st);
+            if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true, 4>(a, st);
+            if (a.N % 64 == 0) return launch_conv_cfg<6, 2, 2, 2, STAGE, EPI, G, true, 4>(a, st);
             if (a.N % 32 == 0) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);   // N = 32, 96, 160 ...
         }
         return CISTA_ERR_UNSUPPORTED;
@@ -517,10 +462,6 @@ int run_layer(const Frame &f, int layer, int it = 0) {
     const bool zstack = f.zl && f.cfg->depth > 0;
     float *z_in = zstack ? f.zl + (size_t)it * hw * 2 * f.C : f.z;
     float *z_out = zstack && it + 1 < f.cfg->depth ? f.zl + (size_t)(it + 1) * hw * 2 * f.C : f.z;
-#ifdef CISTA_EXP_ZOUT
-    // timing experiment (results wrong): ISTA P writes z to scratch instead of in place
-    if (!zstack && f.full) z_out = f.full;
-#endif
     const int C = f.C, B = f.B, h = f.h, w = f.w;
     ConvArgs a;
     switch (layer) {
@@ -903,52 +844,10 @@ struct Bwd {
     Layout L;
     int B, H, W, h, w, C;
     hipStream_t st;
-    hipStream_t wst;        // the stream the weight gradients run on (st, or the side stream)
-    hipEvent_t evf, evj;    // fork / join events of the side stream
     BwdWs ws;
     int slot;   // |max| slot set (rotating over 8)
     int pair;   // next scale pair of the call (never reused within a call)
 };
-
-// The weight gradients (wgrad + partial reduction) of a layer depend on its output gradient and
-// input only, and nothing on the backward's critical path (the dgrad chain) reads them, so they run
-// on a side stream: a one-round dgrad launch at B = 8 (one workgroup lifetime of staging, MFMAs and
-// stores, all workgroups in the same phase) then overlaps the previous layer's wgrad.  fork: the
-// side stream waits for everything the main stream has issued (the gradient, its scale); join: the
-// main stream waits for every weight gradient issued so far (before a buffer they read is reused,
-// and at the end of the call, so the call is stream-ordered for its caller).  One side stream and
-// event pair per host thread and device (created once, reentrant ABI).
-#ifndef CISTA_WGRAD_SIDE
-#define CISTA_WGRAD_SIDE 0        // 1 measured slower at B = 8 (1614 -> 1567 frames/s: the concurrent kernels contend for LDS and HBM)
-#endif
-struct SideStream { hipStream_t s = nullptr; hipEvent_t f = nullptr, j = nullptr; int dev = -1; };
-int side_stream(Bwd &k) {
-    k.wst = k.st; k.evf = k.evj = nullptr;
-    if (!CISTA_WGRAD_SIDE) return CISTA_OK;
-    thread_local SideStream ss[8];
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess) return CISTA_ERR_HIP;
-    SideStream &e = ss[dev & 7];
-    if (e.dev != dev) {
-        if (hipStreamCreateWithFlags(&e.s, hipStreamNonBlocking) != hipSuccess ||
-            hipEventCreateWithFlags(&e.f, hipEventDisableTiming) != hipSuccess ||
-            hipEventCreateWithFlags(&e.j, hipEventDisableTiming) != hipSuccess)
-            return CISTA_ERR_HIP;
-        e.dev = dev;
-    }
-    k.wst = e.s; k.evf = e.f; k.evj = e.j;
-    return CISTA_OK;
-}
-int side_fork(Bwd &k) {
-    if (k.wst == k.st) return CISTA_OK;
-    return hipEventRecord(k.evf, k.st) == hipSuccess && hipStreamWaitEvent(k.wst, k.evf, 0) == hipSuccess
-               ? CISTA_OK : CISTA_ERR_HIP;
-}
-int side_join(Bwd &k) {
-    if (k.wst == k.st) return CISTA_OK;
-    return hipEventRecord(k.evj, k.wst) == hipSuccess && hipStreamWaitEvent(k.st, k.evj, 0) == hipSuccess
-               ? CISTA_OK : CISTA_ERR_HIP;
-}
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
 
@@ -997,7 +896,7 @@ const float *scale_of(Bwd &k, float *dst) {
 void reduce_parts_at(Bwd &k, const float *part, const float *bpart, int ns, long n, float *dst, float *db, long nbias,
                      float sign, int accumulate) {
     const long nb = db ? nbias : 0;
-    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.wst, part, ns, n, dst, sign, accumulate,
+    hipLaunchKernelGGL(reduce_partials_kernel, g1d(n + nb), dim3(256), 0, k.st, part, ns, n, dst, sign, accumulate,
                        bpart, nb, db);
 }
 void reduce_parts(Bwd &k, int ns, long n, float *dst, float *db, long nbias, float sign, int accumulate) {
@@ -1030,8 +929,8 @@ int wgrad_inputs(Bwd &k, const float *gx, const float *ev, const float *img, con
     const size_t lds = ((size_t)WI_TP * (C + 16) + (size_t)(nb + 1) * WI_HPX) * 4;
     switch (nb * 2 + (C == 64 ? 1 : 0)) {
 #define WICASE(n)                                                                                      \
-    case 2 * n: hipLaunchKernelGGL((wgrad_in_kernel<n, 1>), dim3(ns), dim3(256), lds, k.wst, a); break;              \
-    case 2 * n + 1: hipLaunchKernelGGL((wgrad_in_kernel<n, 2>), dim3(ns), dim3(256), lds, k.wst, a); break;
+    case 2 * n: hipLaunchKernelGGL((wgrad_in_kernel<n, 1>), dim3(ns), dim3(256), lds, k.st, a); break;              \
+    case 2 * n + 1: hipLaunchKernelGGL((wgrad_in_kernel<n, 2>), dim3(ns), dim3(256), lds, k.st, a); break;
         WICASE(1) WICASE(2) WICASE(3) WICASE(4) WICASE(5) WICASE(6) WICASE(7) WICASE(8)
 #undef WICASE
     }
@@ -1040,9 +939,6 @@ int wgrad_inputs(Bwd &k, const float *gx, const float *ev, const float *img, con
     return hip_ok();
 }
 
-#ifndef CISTA_WGRAD_SPLIT
-#define CISTA_WGRAD_SPLIT 1   // 0: every wgrad on the exact fp32-MFMA kernel (A/B builds)
-#endif
 #ifndef CISTA_WGRAD_TR
 #define CISTA_WGRAD_TR 1      // split-f16 wgrads on wgrad_tr_kernel (0: wgrad_split_kernel, A/B builds)
 #endif
@@ -1095,12 +991,12 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
             if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S2>)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S2>, dim3(nblk, ns), dim3(WT_THREADS), GE::LDS, k.wst, a);
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S2>, dim3(nblk, ns), dim3(WT_THREADS), GE::LDS, k.st, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }
     }
-    if (CISTA_WGRAD_SPLIT && XS == XS_S1 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 &&
+    if (XS == XS_S1 && gsc && Cout % 64 == 0 && Cin % 32 == 0 && Gc % 4 == 0 &&
         Goff % 4 == 0 && x0c % 32 == 0 && x1c % 32 == 0 && Hin == Hout && Win == Wout) {
         a.gscale = gsc;
         a.TH = WS_TH; a.TW = WS_TW;
@@ -1120,7 +1016,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
             ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
             a.nsplit = ns;
             if (!allow_big_lds((const void *)wgrad_tr_kernel<XS_S1>)) return CISTA_ERR_HIP;
-            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S1>, dim3(nblk, ns), dim3(WT_THREADS), WtGeo<XS_S1>::LDS, k.wst, a);
+            hipLaunchKernelGGL(wgrad_tr_kernel<XS_S1>, dim3(nblk, ns), dim3(WT_THREADS), WtGeo<XS_S1>::LDS, k.st, a);
             reduce_parts(k, ns, (long)Cout * Cin * 9, dst, db, Cout, sign, accumulate);
             return hip_ok();
         }
@@ -1131,7 +1027,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         ns = (ntiles + (ntiles + ns - 1) / ns - 1) / ((ntiles + ns - 1) / ns);   // equal tiles per split
         a.nsplit = ns;
         if (!allow_big_lds((const void *)wgrad_split_kernel)) return CISTA_ERR_HIP;
-        hipLaunchKernelGGL(wgrad_split_kernel, dim3(nblk, ns), dim3(256), WS_LDS, k.wst, a);
+        hipLaunchKernelGGL(wgrad_split_kernel, dim3(nblk, ns), dim3(256), WS_LDS, k.st, a);
         const long n = (long)Cout * Cin * 9;
         reduce_parts(k, ns, n, dst, db, Cout, sign, accumulate);
         return hip_ok();
@@ -1145,7 +1041,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         a.nsplit = ns;
         switch (Cin) {
 #define WSCASE(n) \
-    case n: hipLaunchKernelGGL(wgrad_small_kernel<n>, dim3(ns), dim3(256), 0, k.wst, a); break;
+    case n: hipLaunchKernelGGL(wgrad_small_kernel<n>, dim3(ns), dim3(256), 0, k.st, a); break;
             WSCASE(1) WSCASE(2) WSCASE(3) WSCASE(4) WSCASE(5) WSCASE(6) WSCASE(7) WSCASE(8)
 #undef WSCASE
         }
@@ -1164,7 +1060,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
         ns = ns > ntiles ? ntiles : ns;
         ns = ns < 1 ? 1 : ns;
         a.nsplit = ns;
-        hipLaunchKernelGGL(wgrad_c1_kernel, dim3(ncb, ns), dim3(256), 0, k.wst, a);
+        hipLaunchKernelGGL(wgrad_c1_kernel, dim3(ncb, ns), dim3(256), 0, k.st, a);
         const long n = (long)Cin * 9;
         reduce_parts(k, ns, n, dst, db, 1, sign, accumulate);
         return hip_ok();
@@ -1190,7 +1086,7 @@ int wgrad(Bwd &k, const float *G, int Gc, int Goff, int Cout, const float *X0, i
     const size_t lds = ((size_t)((a.TH * a.TW + 3) & ~3) + HP) * 33 * 4;
     auto kern = wgrad_kernel<XS>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
-    hipLaunchKernelGGL(kern, dim3(nblk, ns), dim3(256), lds, k.wst, a);
+    hipLaunchKernelGGL(kern, dim3(nblk, ns), dim3(256), lds, k.st, a);
     const long n = (long)Cout * Cin * 9;
     reduce_parts(k, ns, n, dst, db, Cout, sign, accumulate);
     return hip_ok();
@@ -1295,7 +1191,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
     if (g.g_rec) {
         hipLaunchKernelGGL(sigmoid_bwd_kernel, g1d(HW), dim3(256), 0, st, g.g_rec, io.rec, ws.gpre, HW);
-        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gpre, 1, 0, 1, sv.u, C, nullptr, 0, C, H, W, H, W, pg.final_w, 1.0f, 0, pg.final_b));
         DgradSmallArgs d;
         d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
@@ -1316,9 +1211,7 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         const float *gsu = scale_of(k);
         CHECK_PTR(gsu);
         hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
-        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
-        CHECK(side_join(k));                            // dxpF (its X) is overwritten next
         float *gup = ws.gU;                              // g wrt up(h)
         if (fold_full) {
             gup = ws.dxpF;                               // (B, H, W, C): the dgrad's input gU is still read
@@ -1341,7 +1234,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C, scale_slots(k));
     const float *gsc = scale_of(k);
     CHECK_PTR(gsc);
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
     if (fold_half) {                                // relu(Dg) mask; h_prev's part if wanted
         CHECK(dgrad_fold(k, CV_LSTM, ws.Gl, gsc, fseg(ws.gy, C, 0, 1.0f, FOLD_MASK, const_cast<float *>(sv.y), scale_slots(k)),
@@ -1354,7 +1246,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
     gsc = scale_of(k);
     CHECK_PTR(gsc);
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
     if (fold_half) {                                // g_z + fold
         CHECK(dgrad_fold(k, CV_DG, ws.gy, gsc, fseg(ws.gz, 2 * C, 0, 1.0f, g.g_z ? FOLD_ADD : FOLD_SET, const_cast<float *>(g.g_z)),
@@ -1414,7 +1305,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         float *sP = sclD + 2 * D, *sD = sP + 2;
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclP, D, sP);
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclD, D, sD);
-        CHECK(side_fork(k));
         CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0, pg.P_b, sP,
                            D * B));
         CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, sv.zl, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
@@ -1422,14 +1312,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------
     // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part)
-    CHECK(side_join(k));                                // Gl (the LSTM wgrad's G) is overwritten next
     hipLaunchKernelGGL(lstc_bwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st, (const float *)sv.gi,
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C, scale_slots(k, 0), scale_slots(k, 1));
     gsc = scale_of(k);                                   // Go; Gl's scale is the next slot set
     CHECK_PTR(gsc);
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
                        pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
     const bool want_zp = io.z_prev && g.g_z_prev;
@@ -1444,7 +1332,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
     CHECK_PTR(gsc);
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
                        pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
     if (fold_half) {
@@ -1457,7 +1344,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
     CHECK_PTR(gsc);
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
     if (fold_half) {
         CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
@@ -1477,7 +1363,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         f.need_full = true;
         CHECK(run_layer(f, CISTA_LAYER_INPUT));
     }
-    CHECK(side_fork(k));
     CHECK(wgrad<XS_S2>(k, ws.gx1, C, 0, C, xfull, C, nullptr, 0, C, H, W, h, w, pg.W0_w, 1.0f, 0, pg.W0_b, gsx));
     {
         // padded-domain stride-2 dgrad into dxpF (split-f16 MFMA, the four output phases of a
@@ -1504,12 +1389,10 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
             rc = hip_ok();
         }
         CHECK(rc);
-        CHECK(side_join(k));                            // gxfull overwrites x_full (W0's wgrad X)
         CHECK(fold(k, ws.dxpF, C, 0, gxfull, C, 0, C, H, W, 1.0f, 0, nullptr));
     }
     // ---- 8. We / Wi ----------------------------------------------------------------------------
     const int half = C / 2, nb = k.cfg->num_bins;
-    CHECK(side_fork(k));
     const int rin = wgrad_inputs(k, gxfull, io.events, io.prev_image, pg);
     if (rin != CISTA_ERR_UNSUPPORTED) CHECK(rin);
     else CHECK(wgrad<XS_NCHW>(k, gxfull, C, 0, half, io.events, nb, nullptr, 0, nb, H, W, H, W, pg.We_w, 1.0f, 0, pg.We_b));
@@ -1534,7 +1417,6 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.Cin = nb; d.accumulate = 0;
         hipLaunchKernelGGL(dgrad_small_kernel, g1d(HW * nb), dim3(256), 0, st, d);
     }
-    CHECK(side_join(k));                                // the caller's stream waits for every wgrad
     return hip_ok();
 }
 }  // namespace
@@ -1883,7 +1765,6 @@ int cista_wgrad_ista_p(const cista_config *cfg, int B, int H, int W, const float
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
     k.pair = 0;
-    k.wst = k.st; k.evf = k.evj = nullptr;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     const int C = k.C;
     return wgrad<XS_S1>(k, G, 2 * C, 0, 2 * C, X, C, nullptr, 0, C, k.h, k.w, k.h, k.w, dW, 1.0f, 0, db, gscale,
@@ -1903,7 +1784,6 @@ int cista_wgrad_w0(const cista_config *cfg, int B, int H, int W, const float *G,
     k.ws = carve_bwd(workspace, *cfg, B, H, W);
     k.slot = 0;
     k.pair = 0;
-    k.wst = k.st; k.evf = k.evj = nullptr;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     const int C = k.C;
     return wgrad<XS_S2>(k, G, C, 0, C, X, C, nullptr, 0, C, H, W, k.h, k.w, dW, 1.0f, 0, db, gscale);
@@ -1964,7 +1844,6 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     k.slot = 0;
     k.pair = 0;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
-    CHECK(side_stream(k));
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
     if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
         return CISTA_ERR_HIP;

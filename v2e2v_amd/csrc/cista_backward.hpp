@@ -752,14 +752,9 @@ __global__ __launch_bounds__(256, 2) void wgrad_split_kernel(const WgradArgs a) 
 // 8 x 18 input halo.  Stride 2 (W0): 2 x 16 output pixels (1 K-step) over a 5 x 33 input halo
 // whose columns are stored parity-split (the 17 even columns, then the 16 odd ones), so the
 // input columns 2x + dx - 1 of four consecutive output pixels are four consecutive LDS pixels.
-#ifndef CISTA_WT_MW
-#define CISTA_WT_MW 4     // MFMA waves per workgroup: 4 (32 co x 32 ci each) or 8 (32 co x 16 ci, 3 waves per SIMD; measured slower)
-#endif
-constexpr int WT_NMW = CISTA_WT_MW, WT_THREADS = (CISTA_WT_MW + 4) * 64;
-static_assert(WT_NMW == 4 || WT_NMW == 8, "wgrad_tr MFMA waves");
-#ifndef CISTA_WT_XD
-#define CISTA_WT_XD 1     // MFMA-wave fragment reads this many steps ahead (1 or 2; 2 measured slower)
-#endif
+// 4 MFMA waves (32 co x 32 ci each) + 4 staging waves (8 MFMA waves and two-step-ahead fragment
+// reads measured slower; commit c9c3ef1 has both)
+constexpr int WT_NMW = 4, WT_THREADS = (WT_NMW + 4) * 64;
 #ifndef CISTA_WT_PRIO
 #define CISTA_WT_PRIO 1   // staging waves at s_setprio CISTA_WT_PRIO (1: training 1727-1743 -> 1744-1745 frames/s same-box)
 #endif
@@ -1007,7 +1002,7 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     }
 
     // ---- MFMA waves: 32 co (planes pco, pco + 1) x NV x 16 ci (planes pci .. pci + NV - 1) ----
-    constexpr int NV = WT_NMW == 8 ? 1 : 2, WPC = 4 / NV;          // ci planes per wave, waves per co pair
+    constexpr int NV = 2, WPC = 4 / NV;                            // ci planes per wave, waves per co pair
     const int pco = 2 * (wave / WPC), pci = NV * (wave % WPC);
     const int kg = lane >> 4, rq = (lane >> 2) & 3, rp = lane & 3;   // transposed-read roles
     f32x4 acc[2][NV][9];
@@ -1052,10 +1047,8 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
                 xl[v] = cat_frag(tr_read(Xp, off + 4 * WT_XPL), tr_read(Xp, off + 4 * WT_XPL + R1));
             }
         };
-        // XD = 1: fragments read one step ahead (double buffer); 2: two steps ahead (X triple
-        // buffer, the next K-step's G two taps early), so a read has a whole step (12 MFMAs)
-        // between its issue and the step that uses it even where the scheduler sinks it
-        constexpr int XD = CISTA_WT_XD, NXB = XD + 1, NSTEP = 9 * GE::KS;
+        // fragments read one step ahead (double buffer)
+        constexpr int XD = 1, NXB = XD + 1, NSTEP = 9 * GE::KS;
         f16x8 gh[2][2], gl[2][2], xh[NXB][NV], xl[NXB][NV];
         read_g(0, gh[0], gl[0]);
 #pragma unroll

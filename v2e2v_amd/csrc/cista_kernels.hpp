@@ -33,57 +33,10 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// STAGE_ZP2: dgrad correlation -- zero padding of 2, output on the padded input domain (H+2)
-// Timing-only experiment switches (scripts/ab_layers.sh builds; results are WRONG when on):
-//   CISTA_EXP_NOB      B fragments of tap 0 reused for every tap (no per-tap L2 loads)
-//   CISTA_EXP_NOA      one A fragment per tap reused for every m-tile (no per-m LDS reads)
-//   CISTA_EXP_NOSTAGE  halo staged only for the first K-chunk
-//   CISTA_EXP_NOEPI    epilogue stores skipped
-//   CISTA_EXP_SMALLSTORE  epilogue stores wrapped into a window of (mask + 1) floats
-#ifndef CISTA_EXP_NOB
-#define CISTA_EXP_NOB 0
-#endif
-#ifndef CISTA_EXP_NOA
-#define CISTA_EXP_NOA 0
-#endif
-#ifndef CISTA_EXP_NOSTAGE
-#define CISTA_EXP_NOSTAGE 0
-#endif
-#ifndef CISTA_EXP_NOEPI
-#define CISTA_EXP_NOEPI 0
-#endif
-#ifndef CISTA_EXP_SMALLSTORE
-#define CISTA_EXP_SMALLSTORE 0     // != 0: store offsets masked into a small window (value = mask)
-#endif
-// CISTA_RANGE_CHECK=0 compiles the fp16-range check (and the range pass) out of the staging (A/B)
+// CISTA_RANGE_CHECK=0 compiles the fp16-range check (and the range pass) out of the staging (A/B
+// timing builds only: results are wrong for inputs beyond the fp16 range)
 #ifndef CISTA_RANGE_CHECK
 #define CISTA_RANGE_CHECK 1
-#endif
-// timing experiment: the workgroups of the first dispatch round (blockIdx < 512) sleep a
-// pseudo-random 0 .. CISTA_EXP_JITTER shader cycles before starting (breaks chip-wide lock-step)
-#ifndef CISTA_EXP_JITTER
-#define CISTA_EXP_JITTER 0
-#endif
-// MFMA issue order within an m-tile: 0 = per n-tile the three split products (hh, hl, lh);
-// 1 = per split product all n-tiles (the A operand changes 2 times in 3 NW MFMAs instead of
-// 2 NW times: fewer operand transitions under a clock held by power, MI355X_MICROARCH.md 'DVFS
-// give-back'); every accumulator still sums hh, hl, lh in that order (bit-identical)
-#ifndef CISTA_MFMA_ORDER
-#define CISTA_MFMA_ORDER 0
-#endif
-#ifndef CISTA_AORDER
-#define CISTA_AORDER 0
-#endif
-#ifndef CISTA_RERUN
-#define CISTA_RERUN 1
-#endif
-// A/B switches: CISTA_PRIO=1 raises the wave priority around each tap's MFMA cluster;
-// CISTA_NT=1 makes the epilogue's burst stores non-temporal
-#ifndef CISTA_PRIO
-#define CISTA_PRIO 0
-#endif
-#ifndef CISTA_NT
-#define CISTA_NT 0
 #endif
 // taps of B fragments in flight ahead of the MFMAs in the double-buffered K loop (48-VGPR-
 // accumulator waves; the others keep 1)
@@ -217,7 +170,6 @@ struct ConvArgs {
     FoldSeg fseg[2];
     int fsplit;
     float *fborder;
-    int items;           // persistent launches: (pixel tile, column block) items of the grid
 };
 
 // workgroup-local pixel index p -> tile coordinates; false for the idle lanes (beyond the
@@ -537,26 +489,12 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
     al[0] = smem[4 * HPpad + abase[0] + toff];
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        if (m + 1 < MT_W && !CISTA_EXP_NOA) {
+        if (m + 1 < MT_W) {
             ah[(m + 1) & 1] = smem[abase[m + 1] + toff];
             al[(m + 1) & 1] = smem[4 * HPpad + abase[m + 1] + toff];
-        } else if (m + 1 < MT_W) {
-            ah[(m + 1) & 1] = ah[m & 1];
-            al[(m + 1) & 1] = al[m & 1];
         }
         const f16x8 xh = __builtin_bit_cast(f16x8, ah[m & 1]);
         const f16x8 xl = __builtin_bit_cast(f16x8, al[m & 1]);
-        if constexpr (CISTA_MFMA_ORDER == 1) {
-#pragma unroll
-            for (int n = 0; n < NW; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, __builtin_bit_cast(f16x8, bh[n]), acc[m][n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NW; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, __builtin_bit_cast(f16x8, bl[n]), acc[m][n], 0, 0, 0);
-#pragma unroll
-            for (int n = 0; n < NW; ++n)
-                acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, __builtin_bit_cast(f16x8, bh[n]), acc[m][n], 0, 0, 0);
-        } else {
 #pragma unroll
         for (int n = 0; n < NW; ++n) {
             const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
@@ -565,13 +503,6 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wl, acc[m][n], 0, 0, 0);
             acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wh, acc[m][n], 0, 0, 0);
         }
-        }
-#if CISTA_AORDER
-        // the next m-tile's two A reads go out BEFORE this m-tile's MFMAs (left to itself the
-        // scheduler sinks them below 2/3 of the MFMAs, ~32 cycles before their use)
-        if (m + 1 < MT_W) __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
-        __builtin_amdgcn_sched_group_barrier(0x8, 3 * NW, 0);
-#endif
         __builtin_amdgcn_sched_barrier(0);
     }
 }
@@ -895,67 +826,11 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
 // SV: training variant -- the epilogue also stores the activations the BPTT backward needs
 // (out1 / out2, see ConvArgs); the inference variant has no such stores in its epilogue.
 // OCC: workgroups per CU the register budget is sized for (LDS: the host's tile choice)
-// Persistent mode (PERS): the grid is one workgroup per resident slot and each workgroup walks a
-// range of (pixel tile, column block) items.  The NEXT item's first K-chunk halo is fetched with
-// LDS-DMA (global_load_lds_dwordx4: no VGPRs, so nothing is held across the epilogue) into the
-// second staging image's area while this item's epilogue runs, and split into hi / lo at the
-// next item's start: the per-tile prologue HBM round trip (~9 k cycles of a ~75 k-cycle tile,
-// DESIGN.md 4.7) overlaps the epilogue instead of stalling the next workgroup.  Raw image: piece
-// P = hp * 8 + q (16 B: channels 4q .. 4q+3 of halo pixel hp), lane-linear per wave instruction.
-template <int STAGE, int NWV>
-__device__ __forceinline__ void dma_chunk0(const ConvArgs &a, u32x4 *raw, int tile) {
-    static_assert(STAGE == STAGE_S1, "persistent staging: reflect-padded stride-1 convs");
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    int t = tile;
-    const int tx = t % a.tiles_x;
-    t /= a.tiles_x;
-    const int ty = t % a.tiles_y;
-    const int b = t / a.tiles_y;
-    const int iy0 = ty * a.TH - 1, ix0 = tx * a.TW - 1;
-    const int HWd = a.TW + 2, HP = (a.TH + 2) * HWd, npieces = HP * 8;
-    for (int u = 0; u * NWV * 64 < npieces; ++u) {
-        const int base = (u * NWV + wave) * 64;
-        const int P = base + lane;
-        if (P < npieces) {
-            const int hp = P >> 3, q = P & 7;
-            const int hy = hp / HWd, hx = hp - hy * HWd;
-            const int iy = reflect_clamp(iy0 + hy, a.Hin), ix = reflect_clamp(ix0 + hx, a.Win);
-            const float *g = a.in0 + ((size_t)(b * a.Hin + iy) * a.Win + ix) * a.c0 + 4 * q;
-            __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void *)g,
-                                             (__attribute__((address_space(3))) void *)(raw + base), 16, 0, 0);
-        }
-    }
-}
-
-// raw chunk-0 image (dma_chunk0) -> hi / lo staging image 0, the items of stage_commit
-template <int NI>
-__device__ __forceinline__ void raw_commit(u32x4 *buf, const u32x4 *raw, int HPpad, const int (&hps)[NI],
-                                           const int (&gs)[NI], f16x2 &amax) {
-#pragma unroll
-    for (int u = 0; u < NI; ++u) {
-        if (hps[u] < 0) continue;
-        const float4 v0 = __builtin_bit_cast(float4, raw[hps[u] * 8 + 2 * gs[u]]);
-        const float4 v1 = __builtin_bit_cast(float4, raw[hps[u] * 8 + 2 * gs[u] + 1]);
-        u32x4 hi, lo;
-        split8(v0, v1, hi, lo, amax);
-        buf[gs[u] * HPpad + hps[u]] = hi;
-        buf[(4 + gs[u]) * HPpad + hps[u]] = lo;
-    }
-}
-
 // one (pixel tile, column block) item of the conv (the body of conv3x3_split3, below)
-// from_raw: the item's chunk-0 halo is already in the raw image (PERS); next_item >= 0: DMA the
-// next item's chunk 0 during this item's epilogue (PERS)
-template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI, bool SV, bool PERS>
-__device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsigned witem, bool from_raw,
-                                          int next_item) {
+template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI, bool SV>
+__device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsigned witem) {
     constexpr int NWV = WM * WN, NTH = NWV * 64;           // waves, threads
-    int tid = threadIdx.x;
-    // PERS: an opaque thread id per item, so that nothing thread-derived (halo items, A / B
-    // addresses, the epilogue's channel constants) is hoisted out of the item loop and held
-    // across it (the hoisted values spilled 50-65 VGPRs in the 250-VGPR convs)
-    if constexpr (PERS) asm volatile("" : "+v"(tid));
+    const int tid = threadIdx.x;
     const int lane = tid & 63;
     const int wave = tid >> 6;
     const int wm = wave % WM;
@@ -1049,14 +924,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
         stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg, tid);
-        if (PERS && from_raw) {
-            // chunk 0 arrived by LDS-DMA during the previous item's epilogue (raw image in the
-            // second staging image's area): every wave's DMAs have landed, and every wave is done
-            // with the epilogue's LDS (the first image's area), before the split writes image 0
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
-            raw_commit<NI>(smem, smem + 8 * HPpad, HPpad, shp, sg, amax);
-        } else {
+        {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
             float4 sv0[NI], sv1[NI];
@@ -1090,7 +958,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
             float4 sv0[NI], sv1[NI];
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
-                if (tap + D <= 8 && !CISTA_EXP_NOB) {
+                if (tap + D <= 8) {
                     const u32x4 *wq = wp + (size_t)(tap + D) * tapstride;
 #pragma unroll
                     for (int n = 0; n < NW; ++n) {
@@ -1098,19 +966,13 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                         bl[(tap + D) % (D + 1)][n] = wq[n * 128 + 64];
                     }
                 }
-                if (tap == 0 && more && !CISTA_EXP_NOSTAGE)
+                if (tap == 0 && more)
                     stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
-#if CISTA_PRIO == 1
-                __builtin_amdgcn_s_setprio(1);
-#endif
-                const int slot = CISTA_EXP_NOB ? 0 : tap % (D + 1);
+                const int slot = tap % (D + 1);
                 if (EPI != EPI_PH4 || ((tmask >> tap) & 1))
                     mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
-#if CISTA_PRIO == 1
-                __builtin_amdgcn_s_setprio(0);
-#endif
             }
-            if (more && !CISTA_EXP_NOSTAGE) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg, amax);
+            if (more) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg, amax);
             __syncthreads();
             if (kc < 8) CISTA_STAMP(3 + kc, __builtin_amdgcn_s_memtime());
         }
@@ -1183,7 +1045,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         int anyfl = fl[0];
 #pragma unroll
         for (int w = 1; w < NWV; ++w) anyfl |= fl[w];
-        if (CISTA_RERUN && !a.ascale && anyfl != 0)
+        if (!a.ascale && anyfl != 0)
             insc = range_rerun<MT_W, WM, NW, STAGE, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0, nchunks, kc0, tid);
     }
 
@@ -1305,11 +1167,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     }
     __syncthreads();
     CISTA_STAMP(15, __builtin_amdgcn_s_memtime());
-    // PERS: the next item's chunk 0 into the raw image (the second staging image's area; this
-    // epilogue's LDS is in the first).  Issued after the epilogue's last workgroup barrier: a
-    // barrier would drain it (hipcc waits vmcnt(0) at __syncthreads while an LDS-DMA is in flight)
-    if constexpr (PERS)
-        if (next_item >= 0) dma_chunk0<STAGE, NWV>(a, smem + 8 * HPpad, next_item / (int)((unsigned)a.N / (unsigned)(WN * NW * 16)));
     const int grp = lane >> 4;
     // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
     const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
@@ -1497,19 +1354,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
 #pragma unroll
         for (int it = 0; it < NIT; ++it) {
             const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
-            if (off >= 0 && (CISTA_EXP_NOEPI == 0 || res[m][it].x == 12345.f)) {
-#if CISTA_EXP_SMALLSTORE
-                *(float4 *)(a.out0 + (((unsigned)off + (unsigned)ch) & (unsigned)CISTA_EXP_SMALLSTORE)) = res[m][it];
-#else
-#if CISTA_NT
-                {
-                    const f32x4 r4 = {res[m][it].x, res[m][it].y, res[m][it].z, res[m][it].w};
-                    __builtin_nontemporal_store(r4, (f32x4 *)(a.out0 + (unsigned)off + (unsigned)chst));
-                }
-#else
+            if (off >= 0) {
                 *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst) = res[m][it];
-#endif
-#endif
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
             }
         }
@@ -1519,17 +1365,14 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
 
 // ------------------------------------------------------------------------------------------
 // The conv kernel.  Workgroup = WM x WN waves; one (pixel tile, column block) item per
-// workgroup, or (PERS) a range of items per workgroup (dma_chunk0 above).
+// workgroup.
 // ------------------------------------------------------------------------------------------
 template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI = 0, bool SV = false,
-          int OCC = 2, bool PERS = false>
+          int OCC = 2>
 __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvArgs a) {
     constexpr int NWV = WM * WN;
     static_assert(NWV == 4 || NWV == 8, "4 or 8 waves per workgroup");
     static_assert(NW % G == 0, "a wave must hold whole gate groups");
-    static_assert(!PERS || (STAGE == STAGE_S1 && NI > 0 && EPI != EPI_FOLD && EPI != EPI_PH4 && EPI != EPI_UP_Q &&
-                            EPI != EPI_UP_Q_SAVE && EPI != EPI_UP4_Q && EPI != EPI_UP4_Q_SAVE),
-                  "persistent items: double-buffered stride-1 convs with the generic epilogue");
     extern __shared__ u32x4 smem[];
 #if CISTA_STAMPS
     {
@@ -1541,39 +1384,19 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
         CISTA_STAMP(1, __builtin_amdgcn_s_memtime());
     }
 #endif
-#if CISTA_EXP_JITTER
-    if (blockIdx.x < 512u) {
-        const unsigned hsh = (blockIdx.x * 2654435761u) >> 16;
-        const unsigned long long until = __builtin_amdgcn_s_memtime() + (unsigned long long)(hsh % 1024u) * CISTA_EXP_JITTER / 1024u;
-        while (__builtin_amdgcn_s_memtime() < until) __builtin_amdgcn_s_sleep(4);
-    }
-#endif
-    if constexpr (PERS) {
-        // XCD-aware: workgroup L runs on XCD L % 8 (round-robin dispatch; the grid is a multiple
-        // of 8); XCD x owns a contiguous range of the a.items items, walked by its workgroups in
-        // lock-step strides, so neighbouring tiles run together on one L2
-        const unsigned total = (unsigned)a.items, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
-        const unsigned x0 = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-        const unsigned x1 = x0 + q + (xcd < r ? 1u : 0u), step = gridDim.x >> 3;
-        bool first = true;
-        for (unsigned w = x0 + (L >> 3); w < x1; w += step, first = false)
-            conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV, PERS>(a, smem, w, !first,
-                                                                          w + step < x1 ? (int)(w + step) : -1);
-    } else {
 #if CISTA_XCD
-        // XCD-aware work order: workgroup L runs on XCD L % 8 (round-robin dispatch), so every XCD
-        // is given a contiguous range of (pixel tile, column block) items, the column blocks of a
-        // tile back to back: the halo a tile shares with its column-block siblings and with its
-        // neighbouring tiles is re-read from that XCD's L2 (bijective for any grid size)
-        const unsigned witem = [] {
-            const unsigned total = gridDim.x, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
-            return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
-        }();
+    // XCD-aware work order: workgroup L runs on XCD L % 8 (round-robin dispatch), so every XCD
+    // is given a contiguous range of (pixel tile, column block) items, the column blocks of a
+    // tile back to back: the halo a tile shares with its column-block siblings and with its
+    // neighbouring tiles is re-read from that XCD's L2 (bijective for any grid size)
+    const unsigned witem = [] {
+        const unsigned total = gridDim.x, L = blockIdx.x, xcd = L & 7u, q = total >> 3, r = total & 7u;
+        return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (L >> 3);
+    }();
 #else
-        const unsigned witem = blockIdx.x;
+    const unsigned witem = blockIdx.x;
 #endif
-        conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV, PERS>(a, smem, witem, false, -1);
-    }
+    conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV>(a, smem, witem);
 }
 
 // ------------------------------------------------------------------------------------------

@@ -20,10 +20,18 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+def under_launcher() -> bool:
+    """True when a launcher (torchrun / torch.distributed.run) set up the rank environment --
+    also at --nproc-per-node 1, where the process group still runs (one RCCL rank)."""
+    return "WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ
+
+
 def init(backend: str | None = None, device: torch.device | None = None):
-    """Initialise the default process group when WORLD_SIZE > 1 (MASTER_ADDR=127.0.0.1)."""
+    """Initialise the default process group when WORLD_SIZE > 1, or whenever the process was
+    started by torchrun (WORLD_SIZE set, even to 1: the N=1 point of the scaling run then goes
+    through the same RCCL process group and DDP all-reduce as N=8).  MASTER_ADDR=127.0.0.1."""
     rank, world, local = env_rank()
-    if world > 1 and not dist.is_initialized():
+    if (world > 1 or under_launcher()) and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         backend = backend or ("nccl" if torch.cuda.is_available() else "gloo")
         kw = {"device_id": device} if (backend == "nccl" and device is not None) else {}
@@ -57,3 +65,13 @@ def sum_over_ranks(x: float, device=None) -> float:
 def barrier():
     if dist.is_available() and dist.is_initialized():
         dist.barrier()
+
+
+def active() -> bool:
+    """A process group is up (torchrun, any world size)."""
+    return dist.is_available() and dist.is_initialized()
+
+
+def finalize():
+    if active():
+        dist.destroy_process_group()
