@@ -214,7 +214,7 @@ def test_ddp_c4_b8_per_rank_matches_single_process_b16(tmp_path, golden):
     assert str(r[0]["packed_sha"]) == str(r[1]["packed_sha"])
 
 
-def _worker_nccl1(port, out_dir):
+def _worker_nccl1(_idx, port, out_dir):
     """One RCCL ("nccl") rank at world size 1, as torchrun --nproc-per-node 1 runs bench.py
     --mode train: the DDP-wrapped 3-frame BPTT step must give the unwrapped model's gradients
     bit for bit (the all-reduce over one rank divides by 1)."""

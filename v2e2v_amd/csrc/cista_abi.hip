@@ -242,13 +242,17 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #else
     dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
 #endif
-    // the LDS also holds the epilogue's per-wave transpose tiles (4 waves x 16 x (NW*16+4))
     // the epilogue indexes outputs with 32-bit element offsets (pixel * Cout, x4 for out2)
     // and the double-buffered staging reads inputs with 32-bit element offsets
     if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 || EPI == EPI_PH4 ? 4 : 1) >= (1LL << 31))
         return CISTA_ERR_UNSUPPORTED;
     if ((long long)a.B * a.Hin * a.Win * (a.c0 > a.c1 ? a.c0 : a.c1) >= (1LL << 31)) return CISTA_ERR_UNSUPPORTED;
-    const size_t epi_lds = (size_t)NWV * 16 * (NW * 16 + 4) * 4 + (size_t)MT_W * WM * 16 * 4;
+    // the epilogue's LDS: the pixel table (MT_W x WM x 16 ints), or the final-conv weights of the
+    // upsample epilogues (9 x Cout floats)
+    const size_t epi_lds = (size_t)MT_W * WM * 16 * 4 > (size_t)9 * a.Cout * 4 ? (size_t)MT_W * WM * 16 * 4
+                                                                                 : (size_t)9 * a.Cout * 4;
+    // EPI_FOLD: a wave's columns must lie in one FoldSeg
+    if (EPI == EPI_FOLD && a.fsplit % (NW * 16)) return CISTA_ERR_UNSUPPORTED;
     // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);

@@ -192,6 +192,8 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
     return i > n - 1 ? n - 1 : i;
 }
 
+template <bool B> struct BoolTag { static constexpr bool value = B; };
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
 __device__ __forceinline__ float bilerp(float ly0, float ly1, float lx0, float lx1, float x00, float x01, float x10,
@@ -477,7 +479,12 @@ __device__ __forceinline__ void stage_issue_px(const ConvArgs &a, const float *s
     }
 }
 
-// one tap of one K-chunk: MT_W x NW tiles, 3 split passes each.  Software-pipelined by hand:
+// one tap of one K-chunk: MT_W x NW tiles, 3 split passes each.  Operand order: A = the packed
+// weight fragment (lane l: 8 K-values of output column l % 16), B = the pixel fragment read from
+// the LDS halo image (lane l: 8 K-values of pixel l % 16) -- the two fragments have the same
+// per-lane shape, so no repacking -- and the accumulator holds D = W^T X^T: lane l gets output
+// columns 4 (l / 16) .. + 3 of pixel l % 16, i.e. 4 consecutive channels of one pixel, which is
+// what the epilogue stores (no LDS transpose).  Software-pipelined by hand:
 // the A fragments of m-tile m+1 are read while m's MFMAs run, and sched_barrier stops the
 // compiler from hoisting every LDS read of the tap up front (which spills at 256 VGPRs).
 template <int MT_W, int NW>
@@ -499,9 +506,9 @@ __device__ __forceinline__ void mfma_tap(f32x4 (&acc)[MT_W][NW], const u32x4 *sm
         for (int n = 0; n < NW; ++n) {
             const f16x8 wh = __builtin_bit_cast(f16x8, bh[n]);
             const f16x8 wl = __builtin_bit_cast(f16x8, bl[n]);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wh, acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xh, wl, acc[m][n], 0, 0, 0);
-            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(xl, wh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc[m][n], 0, 0, 0);
+            acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc[m][n], 0, 0, 0);
         }
         __builtin_amdgcn_sched_barrier(0);
     }
@@ -706,23 +713,22 @@ __device__ __forceinline__ void wg_amax_publish(float *red, unsigned *slots, flo
 // (reference: autograd through ReflectionPad2d, base_layers.py ConvLayer) and goes straight to the
 // destination of its column's segment with that segment's mode (FoldSeg); the border-line pixels
 // (P or Q on the pad) go to the compact buffer fborder, from which fold_fix_kernel adds the
-// reflected terms onto input rows 1, Hin-2 and columns 1, Win-2.  Same per-wave LDS transpose,
-// aux-input ring and store order as the generic epilogue below (one aux input per segment).
+// reflected terms onto input rows 1, Hin-2 and columns 1, Win-2.  A lane holds 4 consecutive
+// packed columns (nt0 + n) * 16 + 4 (lane >> 4) of pixel (lane & 15) of each m-tile (mfma_tap's
+// operand order), so every item is a float4 of the accumulators; the wave's NW * 16 columns lie in
+// one segment (the host requires fsplit % (NW * 16) == 0).  acc arrives scaled (ws applied).
 template <int MT_W, int NW, int WM, int NWV>
 __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *smem, f32x4 (&acc)[MT_W][NW], int b,
                                                    int oy0, int ox0, int wm, int nt0) {
-    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    int etid = threadIdx.x;                                  // opaque: nothing hoisted above the K loop
+    asm volatile("" : "+v"(etid));
+    const int lane = etid & 63;
     constexpr int NTH = NWV * 64;
-    constexpr int LDT = NW * 16 + 4;
-    constexpr int CG = NW * 4;                              // 4-channel groups per pixel of the wave
-    constexpr int NIT = 16 * CG / 64;                       // items per lane per m-tile
     constexpr int NPXB = MT_W * WM * 16;
-    static_assert(64 % CG == 0, "a lane's channel group must be the same for every item");
-    float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
-    int *ptab = reinterpret_cast<int *>(smem) + NWV * 16 * LDT;
+    int *ptab = reinterpret_cast<int *>(smem);
     const int n = a.Hin, mw = a.Win, L = 2 * (mw + 2) + 2 * n;
     // ptab: input pixel index (interior), -(compact border index) - 2 (border line), -1 (outside)
-    for (int p = threadIdx.x; p < NPXB; p += NTH) {
+    for (int p = etid; p < NPXB; p += NTH) {
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
@@ -733,56 +739,45 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
         ptab[p] = v;
     }
     __syncthreads();
-    const int grp = lane >> 4, col = lane & 15;
-    const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
-    const int ch = (nt0 + q) * 16 + c4;                     // packed column = input-gradient channel
-    // the lane's segment is fixed (its channel group is the same for every item)
-    const bool s1 = ch >= a.fsplit;
+    const int kq = lane >> 4, pl = lane & 15;
+    const int ch0 = nt0 * 16 + 4 * kq;                      // packed column = input-gradient channel
+    const bool s1 = nt0 * 16 >= a.fsplit;                   // the wave's segment
     float *const dst = s1 ? a.fseg[1].dst : a.fseg[0].dst;
     float *const aux = s1 ? a.fseg[1].aux : a.fseg[0].aux;
     const int Cd = s1 ? a.fseg[1].Cd : a.fseg[0].Cd;
     const int mode = s1 ? a.fseg[1].mode : a.fseg[0].mode;
     const float fs = s1 ? a.fseg[1].scale : a.fseg[0].scale;
-    const int chd = (s1 ? a.fseg[1].dc0 : a.fseg[0].dc0) + ch - (s1 ? a.fsplit : 0);
+    const int chd0 = (s1 ? a.fseg[1].dc0 : a.fseg[0].dc0) + ch0 - (s1 ? a.fsplit : 0);
     const bool has_aux = mode != FOLD_SET && aux != nullptr;
     // branch-free aux reads (a branch makes the compiler drain vmcnt at the join): a lane without
     // an aux input reads fborder[0..3] (valid memory) and ignores it
-    const float *abase = has_aux ? aux + chd : a.fborder;
-    const float4 bias4 = *(const float4 *)(a.bias + ch);
-    auto load_aux = [&](int m, float4 (&A)[NIT]) {
+    const float *abase = has_aux ? aux + chd0 : a.fborder;
+    float4 bias4[NW];
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
-            const unsigned o = has_aux ? (unsigned)(off < 0 ? 0 : off) * (unsigned)Cd : 0u;
-            A[it] = *(const float4 *)(abase + o);
-        }
+    for (int nn = 0; nn < NW; ++nn) bias4[nn] = *(const float4 *)(a.bias + ch0 + 16 * nn);
+    auto load_aux = [&](int m, float4 (&A)[NW]) {
+        const int off = ptab[(wm * MT_W + m) * 16 + pl];
+        const unsigned o = has_aux ? (unsigned)(off < 0 ? 0 : off) * (unsigned)Cd : 0u;
+#pragma unroll
+        for (int nn = 0; nn < NW; ++nn) A[nn] = *(const float4 *)(abase + o + (has_aux ? 16 * nn : 0));
     };
-    constexpr int PD0 = CISTA_AUX_VGPRS / (NIT * 4);
+    constexpr int PD0 = CISTA_AUX_VGPRS / (NW * 4);
     constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
-    float4 ring[PD][NIT];
+    float4 ring[PD][NW];
 #pragma unroll
     for (int d = 0; d < PD; ++d) load_aux(d, ring[d]);
     float mx = 0.0f;
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        float4 (&cur)[NIT] = ring[m % PD];
+        float4 (&cur)[NW] = ring[m % PD];
         asm volatile("" ::: "memory");
+        const int off = ptab[(wm * MT_W + m) * 16 + pl];
+        float4 rm[NW], r2m[NW];
 #pragma unroll
-        for (int nn = 0; nn < NW; ++nn)
-#pragma unroll
-            for (int j = 0; j < 4; ++j) T[(4 * grp + j) * LDT + nn * 16 + col] = acc[m][nn][j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
-        float4 rm[NIT], r2m[NIT];
-        int om[NIT];
-#pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int row = (it * 64 + lane) / CG;
-            const int off = ptab[(wm * MT_W + m) * 16 + row];
-            const float *src = T + row * LDT + q * 16 + c4;
-            const float v[4] = {src[0] + bias4.x, src[1] + bias4.y, src[2] + bias4.z, src[3] + bias4.w};
-            const float *A = reinterpret_cast<const float *>(&cur[it]);
+        for (int nn = 0; nn < NW; ++nn) {
+            const float v[4] = {acc[m][nn][0] + bias4[nn].x, acc[m][nn][1] + bias4[nn].y,
+                                acc[m][nn][2] + bias4[nn].z, acc[m][nn][3] + bias4[nn].w};
+            const float *A = reinterpret_cast<const float *>(&cur[nn]);
             float r[4], r2[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
@@ -791,41 +786,31 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
                 r2[e] = A[e] + f;
                 if (off < 0) r[e] = v[e];                  // border line: the raw padded-domain value
             }
-            rm[it] = make_float4(r[0], r[1], r[2], r[3]);
-            r2m[it] = make_float4(r2[0], r2[1], r2[2], r2[3]);
-            om[it] = off;
-            if (off >= 0) mx = amax4f(mx, rm[it]);
+            rm[nn] = make_float4(r[0], r[1], r[2], r[3]);
+            r2m[nn] = make_float4(r2[0], r2[1], r2[2], r2[3]);
+            if (off >= 0) mx = amax4f(mx, rm[nn]);
         }
         // refill this ring slot before this m-tile's stores (vmcnt is in order)
         if (m + PD < MT_W) load_aux(m + PD, cur);
         asm volatile("" ::: "memory");
+        if (off >= 0) {
+            const unsigned o = (unsigned)off * (unsigned)Cd + (unsigned)chd0;
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int off = om[it];
-            if (off >= 0) {
-                const unsigned o = (unsigned)off * (unsigned)Cd + (unsigned)chd;
-                if (dst) *(float4 *)(dst + o) = rm[it];
-                if (mode == FOLD_DST2 && aux) *(float4 *)(aux + o) = r2m[it];
-            } else if (off <= -2) {
-                *(float4 *)(a.fborder + (unsigned)(-off - 2) * (unsigned)a.N + (unsigned)ch) = rm[it];
+            for (int nn = 0; nn < NW; ++nn) {
+                if (dst) *(float4 *)(dst + o + 16 * nn) = rm[nn];
+                if (mode == FOLD_DST2 && aux) *(float4 *)(aux + o + 16 * nn) = r2m[nn];
             }
+        } else if (off <= -2) {
+#pragma unroll
+            for (int nn = 0; nn < NW; ++nn)
+                *(float4 *)(a.fborder + (unsigned)(-off - 2) * (unsigned)a.N + (unsigned)(ch0 + 16 * nn)) = rm[nn];
         }
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
     }
     float *red = reinterpret_cast<float *>(smem) + a.lds_flag;
     if (a.fseg[0].amax) wg_amax_publish<NWV>(red, a.fseg[0].amax, s1 ? 0.0f : mx);
     if (a.fseg[1].amax) wg_amax_publish<NWV>(red, a.fseg[1].amax, s1 ? mx : 0.0f);
 }
 
-// ------------------------------------------------------------------------------------------
-// The conv kernel.  Workgroup = 4 waves arranged WM (pixels) x WN (channels); a wave owns
-// MT_W 16-pixel m-tiles x NW 16-column n-tiles (acc = MT_W*NW*4 VGPRs).
-// ------------------------------------------------------------------------------------------
-// SV: training variant -- the epilogue also stores the activations the BPTT backward needs
-// (out1 / out2, see ConvArgs); the inference variant has no such stores in its epilogue.
-// OCC: workgroups per CU the register budget is sized for (LDS: the host's tile choice)
 // one (pixel tile, column block) item of the conv (the body of conv3x3_split3, below)
 template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF, int NI, bool SV>
 __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsigned witem) {
@@ -1050,20 +1035,26 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     }
 
     // ---------------------------------- epilogue ----------------------------------------
-    // acc[m][n][j]: pixel row (wm*MT_W+m)*16 + 4*(lane>>4) + j, packed column (nt0+n)*16 + lane&15
-    const int col = lane & 15;
-    const float ws = *a.wscale * (a.ascale ? a.ascale[1] : 1.0f);
-#pragma unroll
-    for (int m = 0; m < MT_W; ++m)
-#pragma unroll
-        for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
+    // acc[m][n][j]: tile pixel (wm*MT_W+m)*16 + (lane & 15), packed column (nt0+n)*16 + 4*(lane>>4) + j.
+    // The MFMA's A operand is the weight fragment and B the pixel fragment (mfma_tap), so a lane's
+    // accumulator is 4 consecutive output channels of one pixel: the epilogue reads its aux inputs
+    // and writes its outputs as float4s straight from / into the accumulators (no LDS transpose)
+    // opaque thread id: nothing the epilogue derives from it (pixel coordinates, channel offsets)
+    // is hoisted above the K loop and held across it (that spilled)
+    int etid = tid;
+    asm volatile("" : "+v"(etid));
+    const int kq = (etid & 63) >> 4, pl = etid & 15;
+    float ws = *a.wscale * (a.ascale ? a.ascale[1] : 1.0f);
     if (__builtin_expect(insc != 1.0f, 0)) {           // the range pass's pre-scale, up to 2^126
-        const float iv = 1.0f / insc;                  // (a separate step: ws * iv may overflow)
+        const float iv = 1.0f / insc;                  // (separate steps: ws * iv may overflow)
 #pragma unroll
         for (int m = 0; m < MT_W; ++m)
 #pragma unroll
-            for (int n = 0; n < NW; ++n) acc[m][n] *= iv;
+            for (int n = 0; n < NW; ++n) acc[m][n] = acc[m][n] * ws * iv;
+        ws = 1.0f;
     }
+    // below, value = acc * ws + bias as one fma: the product by the power of two ws is exact, so
+    // the fma rounds once, like the separate multiply and add
 
     if constexpr (EPI == EPI_UP_Q || EPI == EPI_UP_Q_SAVE || EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE) {
         constexpr bool PH4 = EPI == EPI_UP4_Q || EPI == EPI_UP4_Q_SAVE;
@@ -1074,88 +1065,112 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         const int c0 = PH4 ? nt0 * 16 - phase * a.Cout : nt0 * 16;   // first channel of the wave
         const int Hq = PH4 ? 2 * a.Hout : a.Hout, Wq = PH4 ? 2 * a.Wout : a.Wout;   // q / u planes
         const int pa = phase >> 1, pb = phase & 1;
-        // values v[t*4 + j] (tap t, accumulator row j) of this lane's channel subset, then a
-        // reduce-scatter over the 16 lanes (columns) of each row group: after halving 48 -> 3,
-        // lane `col` holds the channel sums of value indices 3*col .. 3*col+2.
-        float bz[NW];
-#pragma unroll
-        for (int n = 0; n < NW; ++n) bz[n] = a.bias[(nt0 + n) * 16 + col];
         // final_conv's [tap][C] weights staged once in LDS: read from global inside the loop
         // they would be re-fetched after every store (the stores may alias them), each fetch
         // waiting behind the stores before it (vmcnt is in order)
         __syncthreads();                                   // the last chunk's A reads are done
         float *wfs = reinterpret_cast<float *>(smem);
-        for (int i = tid; i < 9 * a.Cout; i += NTH) wfs[i] = a.aux0[i];
+        for (int i = etid; i < 9 * a.Cout; i += NTH) wfs[i] = a.aux0[i];
+        // u = relu(acc * ws + b) in place (and stored for the backward), lane = 4 channels x NW
+        // n-tiles of one pixel
+#pragma unroll
+        for (int n = 0; n < NW; ++n) {
+            const float4 bz = *(const float4 *)(a.bias + (nt0 + n) * 16 + 4 * kq);
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) {
+                acc[m][n][0] = relu_(fmaf(acc[m][n][0], ws, bz.x));
+                acc[m][n][1] = relu_(fmaf(acc[m][n][1], ws, bz.y));
+                acc[m][n][2] = relu_(fmaf(acc[m][n][2], ws, bz.z));
+                acc[m][n][3] = relu_(fmaf(acc[m][n][3], ws, bz.w));
+            }
+        }
+        if constexpr (SAVE_U) {   // keep u for the final_conv / ReLU backward (full-res NHWC)
+#pragma unroll
+            for (int m = 0; m < MT_W; ++m) {
+                int py, px;
+                const bool in = tile_pixel(a, (wm * MT_W + m) * 16 + pl, py, px);
+                if (in && oy0 + py < a.Hout && ox0 + px < a.Wout) {
+                    const int Y = PH4 ? 2 * (oy0 + py) + pa : oy0 + py;
+                    const int X = PH4 ? 2 * (ox0 + px) + pb : ox0 + px;
+                    float *dst = a.out1 + (((size_t)b * Hq + Y) * Wq + X) * a.Cout + c0 + 4 * kq;
+#pragma unroll
+                    for (int n = 0; n < NW; ++n)
+                        *(float4 *)(dst + n * 16) = make_float4(acc[m][n][0], acc[m][n][1], acc[m][n][2], acc[m][n][3]);
+                }
+            }
+        }
         __syncthreads();
+        // q_t = sum_c u_c wf[t][c]: each lane sums its 4 NW channels for MG m-tiles at a time (a
+        // weight float4 read once per (n-tile, tap) serves the group), then the 4 lane groups of a
+        // pixel are reduce-scattered (lane group kq ends with taps 3 kq .. 3 kq + 2)
+        constexpr int MG = 1;      // (2 or 3 m-tiles per weight read spilled 18-80 VGPRs)
 #pragma unroll
-        for (int m = 0; m < MT_W; ++m) {
-            float v[48];
+        for (int m0 = 0; m0 < MT_W; m0 += MG) {
+            float v[MG][12];
 #pragma unroll
-            for (int i = 0; i < 48; ++i) v[i] = 0.0f;
+            for (int g = 0; g < MG; ++g)
+#pragma unroll
+                for (int t = 0; t < 12; ++t) v[g][t] = 0.0f;
+            // opaque per (group, n-tile): the weight reads are neither merged across groups nor all
+            // issued at once (9 x NW float4s held beside the accumulators spilled)
+            int wo = c0 + 4 * kq;
 #pragma unroll
             for (int n = 0; n < NW; ++n) {
-                const float *wf = wfs + c0 + n * 16 + col;
+                asm volatile("" : "+v"(wo));
 #pragma unroll
-                for (int j = 0; j < 4; ++j) {
-                    const float u = relu_(acc[m][n][j] + bz[n]);
-                    if constexpr (SAVE_U) {   // keep u for the final_conv / ReLU backward
-                        int py, px;
-                        const bool in = tile_pixel(a, (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j, py, px);
-                        if (in && oy0 + py < a.Hout && ox0 + px < a.Wout) {
-                            const int Y = PH4 ? 2 * (oy0 + py) + pa : oy0 + py;
-                            const int X = PH4 ? 2 * (ox0 + px) + pb : ox0 + px;
-                            a.out1[(((size_t)b * Hq + Y) * Wq + X) * a.Cout + c0 + n * 16 + col] = u;
-                        }
+                for (int t = 0; t < 9; ++t) {
+                    const float4 w4 = *(const float4 *)(wfs + t * a.Cout + wo + n * 16);
+#pragma unroll
+                    for (int g = 0; g < MG; ++g) {
+                        v[g][t] = fmaf(acc[m0 + g][n][0], w4.x, v[g][t]);
+                        v[g][t] = fmaf(acc[m0 + g][n][1], w4.y, v[g][t]);
+                        v[g][t] = fmaf(acc[m0 + g][n][2], w4.z, v[g][t]);
+                        v[g][t] = fmaf(acc[m0 + g][n][3], w4.w, v[g][t]);
                     }
-#pragma unroll
-                    for (int t = 0; t < 9; ++t) v[t * 4 + j] = fmaf(u, wf[t * a.Cout], v[t * 4 + j]);
                 }
             }
 #pragma unroll
-            for (int o = 8, half = 24; o >= 1; o >>= 1, half >>= 1) {
-                const bool up = (col & o) != 0;
+            for (int g = 0; g < MG; ++g) {
 #pragma unroll
-                for (int i = 0; i < half; ++i) {
-                    const float keep = up ? v[i + half] : v[i];
-                    const float send = up ? v[i] : v[i + half];
-                    v[i] = keep + __shfl_xor(send, o);
+                for (int o = 32, half = 6; o >= 16; o >>= 1, half >>= 1) {
+                    const bool up = (etid & o) != 0;
+#pragma unroll
+                    for (int i = 0; i < half; ++i) {
+                        const float keep = up ? v[g][i + half] : v[g][i];
+                        const float send = up ? v[g][i] : v[g][i + half];
+                        v[g][i] = keep + __shfl_xor(send, o);
+                    }
                 }
-            }
-#pragma unroll
-            for (int r = 0; r < 3; ++r) {
-                const int idx = 3 * col + r;
-                if (idx >= 36) continue;
-                const int t = idx >> 2, j = idx & 3;
                 int py, px;
-                if (!tile_pixel(a, (wm * MT_W + m) * 16 + 4 * (lane >> 4) + j, py, px)) continue;
+                if (!tile_pixel(a, (wm * MT_W + m0 + g) * 16 + pl, py, px)) continue;
                 const int oy = oy0 + py, ox = ox0 + px;
                 if (oy >= a.Hout || ox >= a.Wout) continue;
                 const int Y = PH4 ? 2 * oy + pa : oy, X = PH4 ? 2 * ox + pb : ox;
-                a.out0[(((size_t)b * 9 + t) * Hq + Y) * Wq + X] = v[r];
+#pragma unroll
+                for (int r = 0; r < 3; ++r) {
+                    const int t = 3 * kq + r;
+                    if (t < 9) a.out0[(((size_t)b * 9 + t) * Hq + Y) * Wq + X] = v[g][r];
+                }
             }
         }
         return;
     }
 
     if constexpr (EPI == EPI_FOLD) {
+#pragma unroll
+        for (int m = 0; m < MT_W; ++m)
+#pragma unroll
+            for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
         conv_fold_epilogue<MT_W, NW, WM, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0);
         return;
     }
 
-    // Epilogue through a per-wave LDS transpose: each m-tile's 16 pixels x (NW*16) columns are
-    // written to LDS as [pixel][column] and read back so that a lane owns 4 consecutive
-    // channels of one pixel -> the aux reads and output writes are 16-byte, fully coalesced
-    // (16 lanes = one pixel's 256-byte channel run) instead of 4-byte scattered accesses.
-    // the staging LDS is free from here on (the K loop / range pass ended with a barrier)
-    constexpr int LDT = NW * 16 + 4;                       // padded row: conflict-free writes
-    constexpr int CG = (NW / G) * 4;                       // 4-channel groups per pixel
-    static_assert(64 % CG == 0, "a lane's channel group must be the same for every item");
+    constexpr int NQ = NW / G;                             // 16-channel groups (of all G gates) per lane
     constexpr int NPXB = MT_W * WM * 16;                   // pixels of the workgroup tile
-    float *T = reinterpret_cast<float *>(smem) + wave * 16 * LDT;
     // per-pixel element offset (pixel * Cout) of the output tensors, -1 outside the image:
     // the items below then need no division, no 64-bit math and no bounds arithmetic
-    int *ptab = reinterpret_cast<int *>(smem) + NWV * 16 * LDT;
-    for (int p = tid; p < NPXB; p += NTH) {
+    int *ptab = reinterpret_cast<int *>(smem);
+    for (int p = etid; p < NPXB; p += NTH) {
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
@@ -1167,51 +1182,60 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     }
     __syncthreads();
     CISTA_STAMP(15, __builtin_amdgcn_s_memtime());
-    const int grp = lane >> 4;
-    // the lane's channel group is fixed (64 % CG == 0): bias / lambda loaded once
-    const int cg = lane % CG, q = cg >> 2, c4 = (cg & 3) * 4;
-    const int ch = ((nt0 / G) + q) * 16 + c4;              // channel within a gate
-    // store offset of the lane's channel group within a pixel's outputs (EPI_PH4: the phase's
-    // pixel of the 2 x 2 block and the channel within the phase)
-    const int chst = EPI == EPI_PH4 ? (((ch / a.Cout) >> 1) * 2 * a.Wout + ((ch / a.Cout) & 1)) * a.Cout + ch % a.Cout
-                                    : ch;
-    float4 bias4[G];
+    // channel (within a gate) of the lane's group q: ch0 + 16 q
+    const int ch0 = (nt0 / G) * 16 + 4 * kq;
+    // store offset of a channel within a pixel's outputs (EPI_PH4: the phase's pixel of the 2 x 2
+    // block and the channel within the phase)
+    auto chst = [&](int ch) {
+        return EPI == EPI_PH4 ? (((ch / a.Cout) >> 1) * 2 * a.Wout + ((ch / a.Cout) & 1)) * a.Cout + ch % a.Cout : ch;
+    };
+    float4 bias4[NQ][G];
 #pragma unroll
-    for (int g = 0; g < G; ++g) bias4[g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + c4);
-    float4 lam4 = make_float4(0.f, 0.f, 0.f, 0.f);
-    if constexpr (EPI == EPI_ISTA_P) lam4 = *(const float4 *)(a.lambda + ch);
+    for (int q = 0; q < NQ; ++q)
+#pragma unroll
+        for (int g = 0; g < G; ++g) bias4[q][g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + 4 * kq);
+    float4 lam4[EPI == EPI_ISTA_P ? NQ : 1];
+    bool lam_nonneg = false;
+    if constexpr (EPI == EPI_ISTA_P) {
+        bool nn = true;
+#pragma unroll
+        for (int q = 0; q < NQ; ++q) {
+            lam4[q] = *(const float4 *)(a.lambda + ch0 + 16 * q);
+            nn = nn && lam4[q].x >= 0.0f && lam4[q].y >= 0.0f && lam4[q].z >= 0.0f && lam4[q].w >= 0.0f;
+        }
+        lam_nonneg = __builtin_amdgcn_ballot_w64(!nn) == 0;    // wave-uniform
+    }
     // aux inputs of m-tile m+1 are loaded before m-tile m's stores go out: vmcnt counts loads
     // and stores in order, so a load issued after a store would also wait for that store (and
     // ISTA_P updates z in place, so the compiler may not reorder them itself)
-    constexpr int NIT = 16 * CG / 64;                      // items per lane per m-tile
     constexpr bool USE_A0 = EPI == EPI_ISTA_D || EPI == EPI_ISTA_P || EPI == EPI_LSTC_OUT ||
                             EPI == EPI_LSTC_CELL || EPI == EPI_LSTM;
     constexpr bool USE_A1 = EPI == EPI_LSTC_CELL;
-    auto load_aux = [&](int m, float4 (&A0)[NIT], float4 (&A1)[NIT]) {
+    auto load_aux = [&](int m, float4 (&A0)[NQ], float4 (&A1)[NQ]) {
+        const int off = ptab[(wm * MT_W + m) * 16 + pl];
+        const unsigned o = (unsigned)(off < 0 ? 0 : off) + (unsigned)ch0;
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
-            const unsigned o = (unsigned)(off < 0 ? 0 : off) + (unsigned)ch;
-            A0[it] = A1[it] = make_float4(0.f, 0.f, 0.f, 0.f);
+        for (int q = 0; q < NQ; ++q) {
+            A0[q] = A1[q] = make_float4(0.f, 0.f, 0.f, 0.f);
             if constexpr (USE_A0) {
                 // branch-free: a NULL aux0 (a None state) reads out0 instead and is zeroed by a
                 // select; a branch here makes the compiler drain vmcnt at the join (no prefetch)
                 // aux0 may be NULL only where it is a previous state (c_prev of LSTC / LSTM)
                 const bool has = (EPI != EPI_LSTC_CELL && EPI != EPI_LSTM) || a.aux0 != nullptr;
                 const float *src = has ? a.aux0 : a.out0;          // out0: same layout, valid memory
-                const float4 v = *(const float4 *)(src + o);
-                A0[it] = has ? v : make_float4(0.f, 0.f, 0.f, 0.f);
+                const float4 v = *(const float4 *)(src + o + 16 * q);
+                A0[q] = has ? v : make_float4(0.f, 0.f, 0.f, 0.f);
             }
-            if constexpr (USE_A1) A1[it] = *(const float4 *)(a.aux1 + o);
+            if constexpr (USE_A1) A1[q] = *(const float4 *)(a.aux1 + o + 16 * q);
         }
     };
     // aux ring: the aux inputs of PD m-tiles are in flight at once (issued together, then one
     // m-tile's worth after each m-tile is consumed): under load an HBM read takes ~5 us, so a
     // one-ahead prefetch made the epilogue a chain of MT_W round trips (scripts/stamps.py)
-    constexpr int AUXV = NIT * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
+    constexpr int AUXV = NQ * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
     constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / (AUXV ? AUXV : 1) : MT_W;   // 8 waves: 128-VGPR budget
     constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
-    float4 ringA0[PD][NIT], ringA1[PD][NIT];
+    float4 ringA0[PD][NQ], ringA1[PD][NQ];
 #pragma unroll
     for (int d = 0; d < PD; ++d) load_aux(d, ringA0[d], ringA1[d]);
     // results are kept in registers (acc[m]'s registers die as res[m] is born) and stored in
@@ -1219,146 +1243,142 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     // the LSTC epilogues (long-K gates convs, MT_W = 12) store in the loop instead: their
     // result registers would not fit next to the accumulators without spilling
     constexpr bool BURST = EPI != EPI_LSTC_CELL && EPI != EPI_LSTC_OUT && NWV == 4;
-    float4 res[BURST ? MT_W : 1][NIT];
-    float4 res1[EPI == EPI_LSTM ? MT_W : 1][NIT];         // EPI_LSTM: the cell state c (out1)
+    float4 res[BURST ? MT_W : 1][NQ];
+    float4 res1[EPI == EPI_LSTM ? MT_W : 1][NQ];          // EPI_LSTM: the cell state c (out1)
+    // the m-tile loop, instantiated twice for ISTA P: FAST (every lambda of the wave >= 0) takes
+    // softshrink as x - med3(x, -l, l), which equals relu(x - l) - relu(-x - l) bit for bit when
+    // l >= 0 (NaN and inf included); otherwise the reference formula literally
+    auto mloop = [&](auto fast_tag) __attribute__((always_inline)) {
+        constexpr bool FAST = decltype(fast_tag)::value;
 #pragma unroll
     for (int m = 0; m < MT_W; ++m) {
-        float4 (&curA0)[NIT] = ringA0[m % PD];
-        float4 (&curA1)[NIT] = ringA1[m % PD];
-        float4 rm[NIT];                                     // non-burst results of this m-tile
-        int om[NIT];
+        float4 (&curA0)[NQ] = ringA0[m % PD];
+        float4 (&curA1)[NQ] = ringA1[m % PD];
+        float4 rm[NQ];                                      // non-burst results of this m-tile
         // compiler-only barrier: keeps the ring exactly PD m-tiles ahead (hoisting every m-tile's
         // loads to the top costs MT_W x AUXV VGPRs and spills)
         asm volatile("" ::: "memory");
+        // items outside the image compute on a clamped (valid) offset and are only skipped by
+        // the stores: no divergent branch, so no vmcnt drain at a join point
+        const int off_raw = ptab[(wm * MT_W + m) * 16 + pl];
+        const int off = off_raw < 0 ? 0 : off_raw;
 #pragma unroll
-        for (int n = 0; n < NW; ++n)
+        for (int q = 0; q < NQ; ++q) {
+            float vv[4 * G];
 #pragma unroll
-            for (int j = 0; j < 4; ++j) T[(4 * grp + j) * LDT + n * 16 + col] = acc[m][n][j];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+            for (int g = 0; g < G; ++g) {
+                const f32x4 ac = acc[m][q * G + g];
+                vv[4 * g + 0] = fmaf(ac[0], ws, bias4[q][g].x);
+                vv[4 * g + 1] = fmaf(ac[1], ws, bias4[q][g].y);
+                vv[4 * g + 2] = fmaf(ac[2], ws, bias4[q][g].z);
+                vv[4 * g + 3] = fmaf(ac[3], ws, bias4[q][g].w);
+            }
+            const unsigned o = (unsigned)off + (unsigned)(ch0 + 16 * q);
+            float r[4], r1[4];
+            if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_PH4) {
 #pragma unroll
-        for (int it0 = 0; it0 < 16 * CG; it0 += 64) {
-            {
-                const int row = (it0 + lane) / CG;
-                // items outside the image compute on a clamped (valid) offset and are only skipped
-                // by the stores: no divergent branch, so no vmcnt drain at a join point
-                const int off_raw = ptab[(wm * MT_W + m) * 16 + row];
-                const int off = off_raw < 0 ? 0 : off_raw;
-                {
-                    float4 v[G];
+                for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? relu_(vv[e]) : vv[e];
+            } else if constexpr (EPI == EPI_ISTA_D) {
+                const float4 x1 = curA0[q];
+                const float *xx = reinterpret_cast<const float *>(&x1);
 #pragma unroll
-                    for (int g = 0; g < G; ++g) {
-                        const float *src = T + row * LDT + (q * G + g) * 16 + c4;
-                        v[g] = make_float4(src[0] + bias4[g].x, src[1] + bias4[g].y, src[2] + bias4[g].z,
-                                           src[3] + bias4[g].w);
-                    }
-                    const unsigned o = (unsigned)off + (unsigned)ch;
-                    float r[4], r1[4];
-                    const float *vv = reinterpret_cast<const float *>(v);
-                    if constexpr (EPI == EPI_BIAS || EPI == EPI_RELU || EPI == EPI_PH4) {
+                for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
+            } else if constexpr (EPI == EPI_ISTA_P) {
+                const float4 z = curA0[q];
+                const float *zz = reinterpret_cast<const float *>(&z);
+                const float *ll = reinterpret_cast<const float *>(&lam4[q]);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) r[e] = EPI == EPI_RELU ? relu_(vv[e]) : vv[e];
-                    } else if constexpr (EPI == EPI_ISTA_D) {
-                        const float4 x1 = curA0[it0 / 64];
-                        const float *xx = reinterpret_cast<const float *>(&x1);
+                for (int e = 0; e < 4; ++e) {
+                    const float x = vv[e] + zz[e];
+                    r1[e] = x;
+                    r[e] = FAST ? x - __builtin_amdgcn_fmed3f(x, -ll[e], ll[e]) : softshrink_(x, ll[e]);
+                }
+                if constexpr (SV)
+                    if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+            } else if constexpr (EPI == EPI_LSTC_OUT) {
+                const float4 c = curA0[q];
+                const float *cc = reinterpret_cast<const float *>(&c);
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
-                    } else if constexpr (EPI == EPI_ISTA_P) {
-                        const float4 z = curA0[it0 / 64];
-                        const float *zz = reinterpret_cast<const float *>(&z);
-                        const float *ll = reinterpret_cast<const float *>(&lam4);
+                for (int e = 0; e < 4; ++e) {
+                    r1[e] = sigmoidf_(vv[e]);
+                    r[e] = r1[e] * tanhf(cc[e]);
+                }
+                if constexpr (SV)
+                    if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
+            } else if constexpr (EPI == EPI_LSTC_CELL) {
+                // packed n-tile order per channel block: (in, forget)
+                const float4 z0 = curA1[q];
+                const float4 cp = curA0[q];
+                const float *zz = reinterpret_cast<const float *>(&z0);
+                const float *pp = reinterpret_cast<const float *>(&cp);
+                float si[4], sf[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            const float x = vv[e] + zz[e];
-                            r1[e] = x;
-                            r[e] = softshrink_(x, ll[e]);
-                        }
-                        if constexpr (SV)
-                            if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
-                    } else if constexpr (EPI == EPI_LSTC_OUT) {
-                        const float4 c = curA0[it0 / 64];
-                        const float *cc = reinterpret_cast<const float *>(&c);
+                for (int e = 0; e < 4; ++e) {
+                    si[e] = sigmoidf_(vv[e]);
+                    sf[e] = sigmoidf_(vv[4 + e]);
+                    r[e] = sf[e] * pp[e] + si[e] * zz[e];
+                }
+                if (SV && off_raw >= 0) {
+                    *(float4 *)(a.out1 + o) = make_float4(si[0], si[1], si[2], si[3]);
+                    *(float4 *)(a.out2 + o) = make_float4(sf[0], sf[1], sf[2], sf[3]);
+                }
+            } else if constexpr (EPI == EPI_LSTM) {
+                // packed n-tile order per channel block: (in, remember, out, cell)
+                const float4 cp = curA0[q];
+                const float *pp = reinterpret_cast<const float *>(&cp);
+                float gi[4], gr[4], go[4], gg[4];
 #pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            r1[e] = sigmoidf_(vv[e]);
-                            r[e] = r1[e] * tanhf(cc[e]);
-                        }
-                        if constexpr (SV)
-                            if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
-                    } else if constexpr (EPI == EPI_LSTC_CELL) {
-                        // packed n-tile order per channel block: (in, forget)
-                        const float4 z0 = curA1[it0 / 64];
-                        const float4 cp = curA0[it0 / 64];
-                        const float *zz = reinterpret_cast<const float *>(&z0);
-                        const float *pp = reinterpret_cast<const float *>(&cp);
-                        float si[4], sf[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            si[e] = sigmoidf_(vv[e]);
-                            sf[e] = sigmoidf_(vv[4 + e]);
-                            r[e] = sf[e] * pp[e] + si[e] * zz[e];
-                        }
-                        if (SV && off_raw >= 0) {
-                            *(float4 *)(a.out1 + o) = make_float4(si[0], si[1], si[2], si[3]);
-                            *(float4 *)(a.out2 + o) = make_float4(sf[0], sf[1], sf[2], sf[3]);
-                        }
-                    } else if constexpr (EPI == EPI_LSTM) {
-                        // packed n-tile order per channel block: (in, remember, out, cell)
-                        const float4 cp = curA0[it0 / 64];
-                        const float *pp = reinterpret_cast<const float *>(&cp);
-                        float gi[4], gr[4], go[4], gg[4];
-#pragma unroll
-                        for (int e = 0; e < 4; ++e) {
-                            gi[e] = sigmoidf_(vv[e]);
-                            gr[e] = sigmoidf_(vv[4 + e]);
-                            go[e] = sigmoidf_(vv[8 + e]);
-                            gg[e] = tanhf(vv[12 + e]);
-                            const float c = gr[e] * pp[e] + gi[e] * gg[e];
-                            r1[e] = c;
-                            r[e] = go[e] * tanhf(c);
-                        }
-                        res1[m][it0 / 64] = make_float4(r1[0], r1[1], r1[2], r1[3]);   // c, stored in the burst
-                        if (SV && off_raw >= 0) {
-                            float *gsv = a.out2 + 4u * (unsigned)off + (unsigned)ch;
-                            *(float4 *)(gsv) = make_float4(gi[0], gi[1], gi[2], gi[3]);
-                            *(float4 *)(gsv + a.Cout) = make_float4(gr[0], gr[1], gr[2], gr[3]);
-                            *(float4 *)(gsv + 2 * a.Cout) = make_float4(go[0], go[1], go[2], go[3]);
-                            *(float4 *)(gsv + 3 * a.Cout) = make_float4(gg[0], gg[1], gg[2], gg[3]);
-                        }
-                    }
-                    if constexpr (BURST) res[m][it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
-                    else {
-                        rm[it0 / 64] = make_float4(r[0], r[1], r[2], r[3]);
-                        om[it0 / 64] = off_raw < 0 ? -1 : (int)((unsigned)off + (unsigned)chst);
-                    }
+                for (int e = 0; e < 4; ++e) {
+                    gi[e] = sigmoidf_(vv[e]);
+                    gr[e] = sigmoidf_(vv[4 + e]);
+                    go[e] = sigmoidf_(vv[8 + e]);
+                    gg[e] = tanhf(vv[12 + e]);
+                    const float c = gr[e] * pp[e] + gi[e] * gg[e];
+                    r1[e] = c;
+                    r[e] = go[e] * tanhf(c);
+                }
+                res1[m][q] = make_float4(r1[0], r1[1], r1[2], r1[3]);   // c, stored in the burst
+                if (SV && off_raw >= 0) {
+                    float *gsv = a.out2 + 4u * (unsigned)off + (unsigned)(ch0 + 16 * q);
+                    *(float4 *)(gsv) = make_float4(gi[0], gi[1], gi[2], gi[3]);
+                    *(float4 *)(gsv + a.Cout) = make_float4(gr[0], gr[1], gr[2], gr[3]);
+                    *(float4 *)(gsv + 2 * a.Cout) = make_float4(go[0], go[1], go[2], go[3]);
+                    *(float4 *)(gsv + 3 * a.Cout) = make_float4(gg[0], gg[1], gg[2], gg[3]);
                 }
             }
+            if constexpr (BURST) res[m][q] = make_float4(r[0], r[1], r[2], r[3]);
+            else rm[q] = make_float4(r[0], r[1], r[2], r[3]);
         }
         // this ring slot is consumed: refill it with m-tile m + PD before this m-tile's stores
         // go out (vmcnt is in order: a load issued after a store also waits for the store)
         if (m + PD < MT_W) load_aux(m + PD, curA0, curA1);
         asm volatile("" ::: "memory");
         if constexpr (!BURST)
+            if (off_raw >= 0)
 #pragma unroll
-            for (int it = 0; it < NIT; ++it)
-                if (om[it] >= 0) *(float4 *)(a.out0 + (unsigned)om[it]) = rm[it];
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+                for (int q = 0; q < NQ; ++q) *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst(ch0 + 16 * q)) = rm[q];
     }
     CISTA_STAMP(16, __builtin_amdgcn_s_memtime());
     if constexpr (BURST)
 #pragma unroll
-    for (int m = 0; m < MT_W; ++m)
+    for (int m = 0; m < MT_W; ++m) {
+        const int off = ptab[(wm * MT_W + m) * 16 + pl];
+        if (off >= 0) {
 #pragma unroll
-        for (int it = 0; it < NIT; ++it) {
-            const int off = ptab[(wm * MT_W + m) * 16 + (it * 64 + lane) / CG];
-            if (off >= 0) {
-                *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst) = res[m][it];
-                if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)ch) = res1[m][it];
+            for (int q = 0; q < NQ; ++q) {
+                *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst(ch0 + 16 * q)) = res[m][q];
+                if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)(ch0 + 16 * q)) = res1[m][q];
             }
         }
+    }
+    };
+    if constexpr (EPI == EPI_ISTA_P) {
+        if (lam_nonneg) mloop(BoolTag<true>{});
+        else mloop(BoolTag<false>{});
+    } else {
+        (void)lam_nonneg;
+        mloop(BoolTag<false>{});
+    }
     CISTA_STAMP(12, __builtin_amdgcn_s_memtime());
     CISTA_STAMP(14, __builtin_amdgcn_s_memrealtime());
 }
