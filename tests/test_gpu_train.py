@@ -305,6 +305,55 @@ def test_wgrad_tr_s2_kernel_matches_fp64(xscale):
     assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
 
 
+@pytest.mark.parametrize("stride", [1, 2])
+def test_wgrad_tr_outlier_tiles_then_o1_tiles(stride):
+    """A split of the split-f16 wgrad walks its tiles in order with a per-tile X pre-scale: a tile
+    whose X holds 1e12 outliers is re-staged at 2^-26, and the O(1) tiles the same split walks after
+    it must be staged unscaled again (at 2^-26 an O(1) value is below the smallest fp16 subnormal
+    and vanishes).  The outlier tiles have G = 0, so they add nothing and the expected gradient is
+    O(1); fp64 conv weight gradient as the truth.  Stride 1: the stacked ISTA P launch (the first
+    tile of every split is one of sample 0's, all outlier tiles); stride 2: W0 at 180 x 240, B = 2
+    (3 tiles per split, the first from sample 0's top 60 output rows)."""
+    import ctypes
+    from v2e2v_amd import _lib
+    C = 64
+    L = _lib.lib()
+    g = torch.Generator(device=DEV).manual_seed(8)
+    if stride == 1:
+        D, B, H, W = 5, 2, 180, 240
+        h, w = H // 2, W // 2
+        m = CistaLSTCNet([H, W], base_channels=C, depth=D, num_bins=5).to(DEV)
+        G = torch.rand(D * B, h, w, 2 * C, device=DEV, generator=g) * 2 - 1
+        X = torch.rand(D * B, h, w, C, device=DEV, generator=g) * 2 - 1
+        G[0] = 0.0
+        X[0, ::7, ::9, ::5] = 1e12
+        dW = torch.empty(2 * C, C, 3, 3, device=DEV)
+        db = torch.empty(2 * C, device=DEV)
+        fn, args = L.cista_wgrad_ista_p, (dW, db)
+    else:
+        B, H, W = 2, 180, 240
+        h, w = H // 2, W // 2
+        m = CistaLSTCNet([H, W], base_channels=C, depth=2, num_bins=5).to(DEV)
+        G = torch.rand(B, h, w, C, device=DEV, generator=g) * 2 - 1
+        X = torch.rand(B, H, W, C, device=DEV, generator=g) * 2 - 1
+        G[0, :60] = 0.0
+        X[0, 2:100:7, ::9, ::5] = 1e12          # read only by output rows <= 50 (G = 0 there)
+        dW = torch.empty(C, C, 3, 3, device=DEV)
+        db = torch.empty(C, device=DEV)
+        fn = L.cista_wgrad_w0
+    sc = torch.tensor([8192.0, 1.0 / 8192.0], device=DEV)
+    ws = m.train_workspace(B, H, W, DEV)
+    _lib.check(fn(ctypes.byref(m._cfg()), B, H, W, G.data_ptr(), X.data_ptr(), sc.data_ptr(), dW.data_ptr(),
+                  db.data_ptr(), ws.data_ptr(), ws.numel(), torch.cuda.current_stream().cuda_stream), "wgrad")
+    torch.cuda.synchronize()
+    Gd = G.double().permute(0, 3, 1, 2)
+    Xd = torch.nn.functional.pad(X.double().permute(0, 3, 1, 2), (1, 1, 1, 1), mode="reflect")
+    ref = torch.nn.grad.conv2d_weight(Xd, tuple(dW.shape), Gd, stride=stride)
+    assert float(ref.abs().max()) < 1e4                  # the outliers contribute nothing
+    assert rel_err(dW.double().cpu().numpy(), ref.cpu().numpy()) < 1e-5
+    assert rel_err(db.double().cpu().numpy(), Gd.sum((0, 2, 3)).cpu().numpy()) < 1e-5
+
+
 @pytest.mark.parametrize("H,W,C,NB", [(6, 8, 32, 5), (8, 12, 32, 5), (12, 10, 32, 5), (12, 16, 96, 5), (10, 14, 128, 5),
                                       (8, 8, 256, 5), (16, 20, 64, 1), (12, 16, 32, 8), (14, 18, 64, 3)])
 def test_small_images_bptt_against_fp64_autograd(H, W, C, NB):

@@ -226,6 +226,10 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     a.TH = t.TH;
     a.TW = t.TW;
     a.pitch = t.mseg ? 16 * t.mseg : t.TW;
+    a.rcp_pitch = 1.0f / (float)a.pitch;
+    // small_div's range: halo pixels < 2048, pitch and halo width <= 512
+    if (((t.TH - 1) * S + 3) * ((t.TW - 1) * S + 3) >= 2048 || a.pitch > 512 || (t.TW - 1) * S + 3 > 512)
+        return CISTA_ERR_UNSUPPORTED;
     a.tiles_y = t.ty;
     a.tiles_x = t.tx;
     constexpr int nblk_cols = WN * NW * 16;
@@ -459,6 +463,13 @@ ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int
     return a;
 }
 
+#ifndef CISTA_PROBE
+#define CISTA_PROBE 0     // diagnostic builds (scripts/l2_probe.py): cista_debug_set_ista_p_probe
+#endif
+#if CISTA_PROBE
+unsigned g_probe_mask = 0;   // != 0: ISTA P's z reads / writes wrapped into [0, mask] elements
+#endif
+
 int run_layer(const Frame &f, int layer, int it = 0) {
     const size_t hw = (size_t)f.B * f.h * f.w;
     // training: the ISTA iterates z_0 .. z_{D-1} stay in the saved stack at f.zl (the backward's
@@ -594,6 +605,12 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                           nullptr, 0);
             a.out0 = z_out; a.aux0 = z_in; a.lambda = blob<float>(f.packed, f.L.lambda);
             a.out1 = f.v ? f.v + it * hw * 2 * C : nullptr;
+#if CISTA_PROBE
+            if (g_probe_mask && !f.v) {             // diagnostic build: the L2-window ISTA P
+                a.probe_mask = g_probe_mask;
+                return launch_conv<STAGE_S1, EPI_ISTA_P_L2, 1>(a, f.st);
+            }
+#endif
             return launch_conv<STAGE_S1, EPI_ISTA_P, 1>(a, f.st);
         case CISTA_LAYER_DG:        // y = relu(Dg.conv(z))                      base_layers.py:222
             a = conv_args_f(f, CV_DG, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
@@ -1429,6 +1446,14 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
 extern "C" {
 
 int cista_abi_version(void) { return CISTA_ABI_VERSION; }
+#if CISTA_PROBE
+// diagnostic builds only: every inference ISTA P launch reads and writes z inside its first
+// mask + 1 elements (an L2-resident window of real data; results wrong).  0: off
+int cista_debug_set_ista_p_probe(unsigned mask) {
+    g_probe_mask = mask;
+    return CISTA_OK;
+}
+#endif
 #if CISTA_STAMPS
 // diagnostic builds only: the conv kernels' phase timestamps go to buf (NULL: off)
 int cista_debug_set_stamps(void *buf) {

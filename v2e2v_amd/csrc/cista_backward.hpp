@@ -841,7 +841,11 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     const bool loader = wave >= WT_NMW;        // waves 0 .. NMW-1: MFMAs; the last 4: staging
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
     const float gsc = a.gscale[0];
-    float sx = 1.0f;                           // X pre-scale in force (power of two, <= 1)
+    // X pre-scale, per tile: 1, or for a tile whose |X| would overflow the fp16 hi part a power of
+    // two <= 1 from that tile's own maximum (so one outlier tile does not push the O(1) values of
+    // every later tile towards the fp16 subnormals).  sx: the re-staged tile's scale (loaders) /
+    // the scale the accumulators are in (MFMA waves)
+    float sx = 1.0f;
 
     // ---- staging (loader waves): item (pixel 4 set + sp, channel quad sq of plane sb) ----
     const int lw = wave - WT_NMW;
@@ -889,11 +893,11 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
 #pragma unroll
         for (int u = 0; u < GE::UX; ++u) xv[u] = load_x(b, oy0, ox0, u);
     };
-    auto put_x = [&](_Float16 *Xp, int u, float4 v) __attribute__((always_inline)) {
+    auto put_x = [&](_Float16 *Xp, int u, float4 v, float scale) __attribute__((always_inline)) {
         const int hp = 4 * (lw + 4 * u) + sp;
         if (GE::HP % 16 && hp >= GE::HP) return;
         const int hy = hp / GE::HW, pos = GE::xpos(hy, hp - hy * GE::HW);
-        if (__builtin_expect(sx != 1.0f, 0)) { v.x *= sx; v.y *= sx; v.z *= sx; v.w *= sx; }
+        if (__builtin_expect(scale != 1.0f, 0)) { v.x *= scale; v.y *= scale; v.z *= scale; v.w *= scale; }
         uint2 hi, lo;
         split4(v, hi, lo);
         *reinterpret_cast<uint2 *>(Xp + sb * WT_XPL + pos * 16 + 4 * sq) = hi;
@@ -916,24 +920,22 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
 #pragma unroll
         for (int u = 0; u < GE::UX; ++u) {
             m = fmaxf(m, fmaxf(fmaxf(fabsf(xv[u].x), fabsf(xv[u].y)), fmaxf(fabsf(xv[u].z), fabsf(xv[u].w))));
-            put_x(Xp, u, xv[u]);
+            put_x(Xp, u, xv[u], 1.0f);
         }
-        const bool ovf = m * sx >= 32768.0f && m < 3.0e38f;               // hi part would overflow
+        const bool ovf = m >= 32768.0f && m < 3.0e38f;                    // hi part would overflow
         const bool any = __ballot(ovf ? 1 : 0) != 0;
         if (lane == 0) flag[lw] = any ? 1 : 0;
     };
     // rare path (uniform: every wave read the same flags): the tile in buf is re-staged with a
-    // smaller X pre-scale, the MFMA waves rescale their accumulators exactly.  The loaders re-read
-    // the tile's X one item at a time (their registers hold the next tile's loads in flight).
-    // Both roles pass the same three barriers and derive the same scale from the same maxima.
-    auto new_scale = [&]() __attribute__((always_inline)) {
+    // pre-scale from its own maximum, the MFMA waves rescale their accumulators exactly (and back
+    // at the next unflagged tile).  The loaders re-read the tile's X one item at a time (their
+    // registers hold the next tile's loads in flight).  Both roles pass the same three barriers
+    // and derive the same scale from the same maxima.
+    auto tile_scale = [&]() __attribute__((always_inline)) {
         const float m = fmaxf(fmaxf(xmx[0], xmx[1]), fmaxf(xmx[2], xmx[3]));
         int e = (int)floorf(log2f(16384.0f / m));
-        e = e < -126 ? -126 : e;
-        const float st = fminf(ldexpf(1.0f, e), sx);
-        const float r = st / sx;
-        sx = st;
-        return r;
+        e = e < -126 ? -126 : (e > 0 ? 0 : e);
+        return ldexpf(1.0f, e);
     };
     auto acc_zero = [](auto &acc) __attribute__((always_inline)) {
 #pragma unroll
@@ -979,9 +981,9 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
                 for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
                 if (lane == 0) xmx[lw] = m;
                 __syncthreads();
-                new_scale();
+                sx = tile_scale();
 #pragma unroll 1
-                for (int u = 0; u < GE::UX; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u));
+                for (int u = 0; u < GE::UX; ++u) put_x(sm + bi * WT_BUF + 8 * WT_GPL, u, load_x(b, oy0, ox0, u), sx);
                 __syncthreads();
             }
             if (tile + a.nsplit < ntiles) {
@@ -1014,17 +1016,25 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     int it = 0;
     for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
         const int bi = it & 1;
-        if (__builtin_expect(flagged(bi), 0)) {
-            __syncthreads();
-            __syncthreads();
-            const float r = new_scale();
+        // the tile's X scale: from its own maximum when flagged, else 1 (powers of two, so the
+        // accumulator rescale by r is exact)
+        const bool fl = flagged(bi);
+        if (__builtin_expect(fl || sx != 1.0f, 0)) {    // uniform rare path
+            float st = 1.0f;
+            if (fl) {
+                __syncthreads();
+                __syncthreads();
+                st = tile_scale();
+            }
+            const float r = st / sx;
+            sx = st;
 #pragma unroll
             for (int u = 0; u < 2; ++u)
 #pragma unroll
                 for (int v = 0; v < NV; ++v)
 #pragma unroll
                     for (int t = 0; t < 9; ++t) acc[u][v][t] *= r;
-            __syncthreads();
+            if (fl) __syncthreads();
         }
         const _Float16 *Gp = sm + bi * WT_BUF, *Xp = Gp + 8 * WT_GPL;
         // 27 (K-step, tap) steps, software-pipelined: the fragments of step n + 1 are read before
@@ -1830,7 +1840,7 @@ __global__ void lstm_bwd_kernel(const float *gates, const float *c, const float 
     const float i = gt[ch], r = gt[C + ch], o = gt[2 * C + ch], g = gt[3 * C + ch];
     const float cc = c[idx];
     const float cp = c_prev ? c_prev[idx] : 0.0f;
-    const float th = tanhf(cc);
+    const float th = gate_tanh(cc);
     const float dh = gh ? gh[idx] : 0.0f;
     const float dc = (gc ? gc[idx] : 0.0f) + dh * o * (1.0f - th * th);
     float *Gp = G + p * 4 * C;
@@ -1952,7 +1962,7 @@ __global__ void lstc_bwd_kernel(const float *gi_, const float *gf_, const float 
     const long p = idx / Cz;
     const int ch = (int)(idx % Cz);
     const float i = gi_[idx], f = gf_[idx], o = go_[idx];
-    const float cc = c[idx], th = tanhf(cc);
+    const float cc = c[idx], th = gate_tanh(cc);
     const float cp = c_prev ? c_prev[idx] : 0.0f;
     const float dz = gz[idx];
     const float dc = (gcl ? gcl[idx] : 0.0f) + dz * o * (1.0f - th * th);

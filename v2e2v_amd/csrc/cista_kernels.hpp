@@ -99,6 +99,9 @@ enum Epi {
                          // packed column = (phase a*2+b, channel); phase-grid pixel (i, j) is the
                          // padded-domain input-gradient pixel (2i+a, 2j+b) of a (2 Hout, 2 Wout)
                          // NHWC tensor; a wave skips the taps its phase has no weight on
+    EPI_ISTA_P_L2 = 13,  // diagnostic builds only (CISTA_PROBE=1, scripts/l2_probe.py): EPI_ISTA_P with the
+                         // z aux reads and z writes wrapped into a small L2-resident window
+                         // (offset & probe_mask) -- timing only, results wrong
     EPI_FOLD = 12        // training dgrad (STAGE_ZP2) with the reflect fold in the epilogue: a
                          // padded-domain output pixel (P, Q) inside [1, Hin] x [1, Win] IS the
                          // input gradient at (P-1, Q-1) up to the reflected border sources, and is
@@ -165,17 +168,25 @@ struct ConvArgs {
     // m-tile partly idle), so the 16 lanes of an m-tile read 16 contiguous halo slots -- one
     // conflict-free ds_read_b128 lane group -- also when TW % 16 != 0
     int pitch;
+    float rcp_pitch;     // 1 / pitch (small_div)
     // EPI_FOLD: packed columns [0, fsplit) -> fseg[0], [fsplit, N) -> fseg[1]; the padded border
     // lines (B, 2 (Win+2) + 2 Hin, N) -> fborder (fold_border_index)
     FoldSeg fseg[2];
     int fsplit;
     float *fborder;
+    unsigned probe_mask; // EPI_ISTA_P_L2 only
 };
+
+// floor(n / d) for 0 <= n < 2048 and 1 <= d <= 512 through fp32, given rcp_d = 1 / d correctly
+// rounded: (n + 0.5) / d lies at least 0.5 / d >= 2^-10 from an integer and the fp32 result is
+// within 2^-23 relative (<= 2.5e-4 absolute) of it.  4 VALU instead of the ~12 of a runtime
+// integer division (the conv prologue's per-item halo and per-m-tile pixel coordinates)
+__device__ __forceinline__ int small_div(int n, float rcp_d) { return (int)(((float)n + 0.5f) * rcp_d); }
 
 // workgroup-local pixel index p -> tile coordinates; false for the idle lanes (beyond the
 // tile), whose (py, px) are clamped to a valid pixel
 __device__ __forceinline__ bool tile_pixel(const ConvArgs &a, int p, int &py, int &px) {
-    py = p / a.pitch;
+    py = small_div(p, a.rcp_pitch);
     px = p - py * a.pitch;
     const bool ok = py < a.TH && px < a.TW;
     py = py < a.TH ? py : a.TH - 1;
@@ -195,6 +206,39 @@ __device__ __forceinline__ int reflect_clamp(int i, int n) {
 template <bool B> struct BoolTag { static constexpr bool value = B; };
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// Gate nonlinearities of the conv epilogues (ConvLSTC / ConvLSTM gates, base_layers.py:57-69,
+// 116-128).  CISTA_FAST_GATES=1: sigmoid = rcp(1 + 2^(-x log2 e)) on v_exp_f32 / v_rcp_f32 (both
+// ~1 ulp) and tanh = sign(x) (1 - e) / (1 + e), e = 2^(-2|x| log2 e), below |x| = 0.125 the odd
+// Taylor polynomial to x^7 (truncation < 2e-10 relative; the exp form would cancel there):
+// ~6 / ~16 VALU against ~25 / ~45 for expf + IEEE division and ocml's branchy tanhf, within ~1e-6
+// relative of them.  NaN propagates, +-inf saturate like the library functions.  The frame's
+// final sigmoid (final_q_kernel) keeps the library path.
+#ifndef CISTA_FAST_GATES
+#define CISTA_FAST_GATES 1
+#endif
+__device__ __forceinline__ float gate_sigmoid(float x) {
+#if CISTA_FAST_GATES
+    const float e = __builtin_amdgcn_exp2f(__fmul_rn(-x, 1.4426950408889634f));
+    return __builtin_amdgcn_rcpf(__fadd_rn(1.0f, e));
+#else
+    return sigmoidf_(x);
+#endif
+}
+__device__ __forceinline__ float gate_tanh(float x) {
+#if CISTA_FAST_GATES
+    const float ax = fabsf(x);
+    const float e = __builtin_amdgcn_exp2f(__fmul_rn(ax, -2.8853900817779268f));       // e^(-2|x|)
+    const float big = __fmul_rn(__fsub_rn(1.0f, e), __builtin_amdgcn_rcpf(__fadd_rn(1.0f, e)));
+    const float x2 = __fmul_rn(x, x);
+    // x (1 - x^2/3 + 2 x^4/15 - 17 x^6/315)
+    const float p = fmaf(fmaf(fmaf(x2, -0.053968254f, 0.13333334f), x2, -0.33333334f), x2, 1.0f);
+    const float small = __fmul_rn(x, p);
+    return ax < 0.125f ? small : __builtin_copysignf(big, x);
+#else
+    return tanhf(x);
+#endif
+}
 
 __device__ __forceinline__ float bilerp(float ly0, float ly1, float lx0, float lx1, float x00, float x01, float x10,
                                         float x11) {
@@ -404,6 +448,7 @@ template <int STAGE, int NI, int NT = 256>
 __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, int ix0, int HH, int HWd,
                                              int (&spix)[NI], int (&hps)[NI], int (&gs)[NI], int tid) {
     const int HP = HH * HWd;
+    const float rcp_hwd = 1.0f / (float)HWd;
     const int nitems = ((HP + 7) & ~7) * 4;
 #pragma unroll
     for (int u = 0; u < NI; ++u) {
@@ -411,7 +456,7 @@ __device__ __forceinline__ void stage_pixels(const ConvArgs &a, int b, int iy0, 
         const int hp = ((it >> 5) << 3) | (it & 7);
         gs[u] = (it >> 3) & 3;
         hps[u] = (it < nitems && hp < HP) ? hp : -1;
-        const int hy = hp / HWd, hx = hp - (hp / HWd) * HWd;
+        const int hy = small_div(hp, rcp_hwd), hx = hp - hy * HWd;
         int pix = -1;
         if (hps[u] >= 0) {
             if constexpr (STAGE == STAGE_ZP2) {
@@ -781,9 +826,9 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
             float r[4], r2[4];
 #pragma unroll
             for (int e = 0; e < 4; ++e) {
-                const float f = v[e] * fs;
-                r[e] = mode == FOLD_ADD ? A[e] + f : (mode == FOLD_MASK ? (A[e] > 0.0f ? f : 0.0f) : f);
-                r2[e] = A[e] + f;
+                const float f = __fmul_rn(v[e], fs);
+                r[e] = mode == FOLD_ADD ? __fadd_rn(A[e], f) : (mode == FOLD_MASK ? (A[e] > 0.0f ? f : 0.0f) : f);
+                r2[e] = __fadd_rn(A[e], f);
                 if (off < 0) r[e] = v[e];                  // border line: the raw padded-domain value
             }
             rm[nn] = make_float4(r[0], r[1], r[2], r[3]);
@@ -890,6 +935,18 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         segC = kc < kc0 ? a.c0 : a.c1;
         choff = (kc < kc0 ? kc : kc - kc0) * 32;
     };
+    // geometry of the generic epilogue's aux-input ring (below)
+    constexpr int NQ = NW / G;                             // 16-channel groups (of all G gates) per lane
+    constexpr bool ISTAP = EPI == EPI_ISTA_P || EPI == EPI_ISTA_P_L2;
+    // EPI_ISTA_P_L2 (diagnostic): aux / output element offsets wrapped into the probe window
+    auto wrap = [&](unsigned o) { return EPI == EPI_ISTA_P_L2 ? (o & a.probe_mask) : o; };
+    constexpr bool USE_A0 = EPI == EPI_ISTA_D || ISTAP || EPI == EPI_LSTC_OUT ||
+                            EPI == EPI_LSTC_CELL || EPI == EPI_LSTM;
+    constexpr bool USE_A1 = EPI == EPI_LSTC_CELL;
+    constexpr int AUXV = NQ * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
+    constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / (AUXV ? AUXV : 1) : MT_W;   // 8 waves: 128-VGPR budget
+    constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
+    float4 ringA0[PD][NQ], ringA1[PD][NQ];
     float insc = 1.0f;   // the range pass's input pre-scale (1 unless the tile was re-run)
     // Range pass.  A staged value whose fp16 hi part overflows (|x| >= 65520, far beyond what
     // the reference's activations reach on normalised voxels, but legal fp32) would make the
@@ -919,9 +976,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         __syncthreads();
         CISTA_STAMP(2, __builtin_amdgcn_s_memtime());
         for (int kc = 0; kc < nchunks; ++kc) {
+            const bool more = kc + 1 < nchunks;
             const u32x4 *cur = smem + (kc & 1) * 8 * HPpad;
             u32x4 *nxt = smem + ((kc + 1) & 1) * 8 * HPpad;
-            const bool more = kc + 1 < nchunks;
             const float *nseg; int nsegC, nchoff;
             seg_of(more ? kc + 1 : kc, nseg, nsegC, nchoff);
 #pragma unroll
@@ -951,8 +1008,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                         bl[(tap + D) % (D + 1)][n] = wq[n * 128 + 64];
                     }
                 }
-                if (tap == 0 && more)
-                    stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
+                if (tap == 0 && more) stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
                 const int slot = tap % (D + 1);
                 if (EPI != EPI_PH4 || ((tmask >> tap) & 1))
                     mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
@@ -1165,7 +1221,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         return;
     }
 
-    constexpr int NQ = NW / G;                             // 16-channel groups (of all G gates) per lane
     constexpr int NPXB = MT_W * WM * 16;                   // pixels of the workgroup tile
     // per-pixel element offset (pixel * Cout) of the output tensors, -1 outside the image:
     // the items below then need no division, no 64-bit math and no bounds arithmetic
@@ -1194,9 +1249,9 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     for (int q = 0; q < NQ; ++q)
 #pragma unroll
         for (int g = 0; g < G; ++g) bias4[q][g] = *(const float4 *)(a.bias + (nt0 + q * G + g) * 16 + 4 * kq);
-    float4 lam4[EPI == EPI_ISTA_P ? NQ : 1];
+    float4 lam4[ISTAP ? NQ : 1];
     bool lam_nonneg = false;
-    if constexpr (EPI == EPI_ISTA_P) {
+    if constexpr (ISTAP) {
         bool nn = true;
 #pragma unroll
         for (int q = 0; q < NQ; ++q) {
@@ -1208,9 +1263,6 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     // aux inputs of m-tile m+1 are loaded before m-tile m's stores go out: vmcnt counts loads
     // and stores in order, so a load issued after a store would also wait for that store (and
     // ISTA_P updates z in place, so the compiler may not reorder them itself)
-    constexpr bool USE_A0 = EPI == EPI_ISTA_D || EPI == EPI_ISTA_P || EPI == EPI_LSTC_OUT ||
-                            EPI == EPI_LSTC_CELL || EPI == EPI_LSTM;
-    constexpr bool USE_A1 = EPI == EPI_LSTC_CELL;
     auto load_aux = [&](int m, float4 (&A0)[NQ], float4 (&A1)[NQ]) {
         const int off = ptab[(wm * MT_W + m) * 16 + pl];
         const unsigned o = (unsigned)(off < 0 ? 0 : off) + (unsigned)ch0;
@@ -1223,19 +1275,16 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 // aux0 may be NULL only where it is a previous state (c_prev of LSTC / LSTM)
                 const bool has = (EPI != EPI_LSTC_CELL && EPI != EPI_LSTM) || a.aux0 != nullptr;
                 const float *src = has ? a.aux0 : a.out0;          // out0: same layout, valid memory
-                const float4 v = *(const float4 *)(src + o + 16 * q);
+                const float4 v = *(const float4 *)(src + wrap(o + 16 * q));
                 A0[q] = has ? v : make_float4(0.f, 0.f, 0.f, 0.f);
             }
             if constexpr (USE_A1) A1[q] = *(const float4 *)(a.aux1 + o + 16 * q);
         }
     };
-    // aux ring: the aux inputs of PD m-tiles are in flight at once (issued together, then one
-    // m-tile's worth after each m-tile is consumed): under load an HBM read takes ~5 us, so a
-    // one-ahead prefetch made the epilogue a chain of MT_W round trips (scripts/stamps.py)
-    constexpr int AUXV = NQ * 4 * ((USE_A0 ? 1 : 0) + (USE_A1 ? 1 : 0));   // VGPRs per m-tile
-    constexpr int PD0 = AUXV ? (NWV == 8 ? 16 : CISTA_AUX_VGPRS) / (AUXV ? AUXV : 1) : MT_W;   // 8 waves: 128-VGPR budget
-    constexpr int PD = PD0 < 1 ? 1 : (PD0 > MT_W ? MT_W : PD0);
-    float4 ringA0[PD][NQ], ringA1[PD][NQ];
+    // aux ring (ringA0 / ringA1, declared before the K loop): the aux inputs of PD m-tiles are in
+    // flight at once (issued together, then one m-tile's worth after each m-tile is consumed):
+    // under load an HBM read takes ~5 us, so a one-ahead prefetch made the epilogue a chain of
+    // MT_W round trips (scripts/stamps.py)
 #pragma unroll
     for (int d = 0; d < PD; ++d) load_aux(d, ringA0[d], ringA1[d]);
     // results are kept in registers (acc[m]'s registers die as res[m] is born) and stored in
@@ -1283,7 +1332,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 const float *xx = reinterpret_cast<const float *>(&x1);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) r[e] = xx[e] - vv[e];
-            } else if constexpr (EPI == EPI_ISTA_P) {
+            } else if constexpr (ISTAP) {
                 const float4 z = curA0[q];
                 const float *zz = reinterpret_cast<const float *>(&z);
                 const float *ll = reinterpret_cast<const float *>(&lam4[q]);
@@ -1300,8 +1349,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 const float *cc = reinterpret_cast<const float *>(&c);
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    r1[e] = sigmoidf_(vv[e]);
-                    r[e] = r1[e] * tanhf(cc[e]);
+                    r1[e] = gate_sigmoid(vv[e]);
+                    r[e] = r1[e] * gate_tanh(cc[e]);
                 }
                 if constexpr (SV)
                     if (off_raw >= 0) *(float4 *)(a.out1 + o) = make_float4(r1[0], r1[1], r1[2], r1[3]);
@@ -1314,9 +1363,11 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 float si[4], sf[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    si[e] = sigmoidf_(vv[e]);
-                    sf[e] = sigmoidf_(vv[4 + e]);
-                    r[e] = sf[e] * pp[e] + si[e] * zz[e];
+                    si[e] = gate_sigmoid(vv[e]);
+                    sf[e] = gate_sigmoid(vv[4 + e]);
+                    // every operation rounded on its own (the reference's order; the compiler may
+                    // not contract it into an fma differently per tile configuration)
+                    r[e] = __fadd_rn(__fmul_rn(sf[e], pp[e]), __fmul_rn(si[e], zz[e]));
                 }
                 if (SV && off_raw >= 0) {
                     *(float4 *)(a.out1 + o) = make_float4(si[0], si[1], si[2], si[3]);
@@ -1329,13 +1380,13 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 float gi[4], gr[4], go[4], gg[4];
 #pragma unroll
                 for (int e = 0; e < 4; ++e) {
-                    gi[e] = sigmoidf_(vv[e]);
-                    gr[e] = sigmoidf_(vv[4 + e]);
-                    go[e] = sigmoidf_(vv[8 + e]);
-                    gg[e] = tanhf(vv[12 + e]);
-                    const float c = gr[e] * pp[e] + gi[e] * gg[e];
+                    gi[e] = gate_sigmoid(vv[e]);
+                    gr[e] = gate_sigmoid(vv[4 + e]);
+                    go[e] = gate_sigmoid(vv[8 + e]);
+                    gg[e] = gate_tanh(vv[12 + e]);
+                    const float c = __fadd_rn(__fmul_rn(gr[e], pp[e]), __fmul_rn(gi[e], gg[e]));
                     r1[e] = c;
-                    r[e] = go[e] * tanhf(c);
+                    r[e] = go[e] * gate_tanh(c);
                 }
                 res1[m][q] = make_float4(r1[0], r1[1], r1[2], r1[3]);   // c, stored in the burst
                 if (SV && off_raw >= 0) {
@@ -1366,13 +1417,13 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         if (off >= 0) {
 #pragma unroll
             for (int q = 0; q < NQ; ++q) {
-                *(float4 *)(a.out0 + (unsigned)off + (unsigned)chst(ch0 + 16 * q)) = res[m][q];
+                *(float4 *)(a.out0 + wrap((unsigned)off + (unsigned)chst(ch0 + 16 * q))) = res[m][q];
                 if constexpr (EPI == EPI_LSTM) *(float4 *)(a.out1 + (unsigned)off + (unsigned)(ch0 + 16 * q)) = res1[m][q];
             }
         }
     }
     };
-    if constexpr (EPI == EPI_ISTA_P) {
+    if constexpr (ISTAP) {
         if (lam_nonneg) mloop(BoolTag<true>{});
         else mloop(BoolTag<false>{});
     } else {
