@@ -3,6 +3,7 @@
 // schedule of CistaLSTCNet.forward (reference e2v/e2v_model.py:41-90).
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <mutex>
@@ -153,9 +154,14 @@ size_t lds_bytes(int TH, int TW, int S) {
 // equal efficiency a layout whose m-tile A-fragment reads are bank-conflict free (each m-tile's
 // 16 lanes in one halo row: ds_read_b128 serves 16 lanes of 16 contiguous slots per cycle),
 // then the smaller LDS image.
-Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ = 2, bool seg = false) {
+// halo_w > 0: rank by cost per useful output pixel instead, tiles x (block_px + halo_w x halo
+// pixels) x (1 + 0.05 if the m-tile reads are bank-conflicted): the training dgrads (2-chunk K
+// loops at B = 8) otherwise took 48 x 2 tiles (96 px, a 200-pixel halo, conflicted reads) for
+// their 96-pixel workgroups
+Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ = 2, bool seg = false,
+                 double halo_w = 0.0) {
     Tile best{1, 1, Hout, Wout, 0, 0};
-    double best_eff = -1.0;
+    double best_eff = -1.0, best_cost = 1e300;
     int best_conf = 1;
     size_t best_lds = ~(size_t)0;
     const size_t lds_cap = 160 * 1024 / occ;   // occ workgroups per CU
@@ -180,10 +186,19 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
         const double eff = (double)Hout * Wout / ((double)ty * tx * block_px);
         // row-major m-tiles that wrap a tile row put two halo rows' slots in one lane group
         const int conf = (S == 1 && (mode || TW % 16 == 0)) ? 0 : 1;
-        const bool better = eff > best_eff + 1e-9 ||
-                            (eff > best_eff - 1e-9 && (conf < best_conf || (conf == best_conf && lds < best_lds)));
+        bool better;
+        double cost = 0.0;
+        if (halo_w > 0.0) {
+            const double hp = (double)((TH - 1) * S + 3) * ((TW - 1) * S + 3);
+            cost = (double)ty * tx * (block_px + halo_w * hp) * (conf ? 1.05 : 1.0) / ((double)Hout * Wout);
+            better = cost < best_cost - 1e-9 || (cost < best_cost + 1e-9 && lds < best_lds);
+        } else {
+            better = eff > best_eff + 1e-9 ||
+                     (eff > best_eff - 1e-9 && (conf < best_conf || (conf == best_conf && lds < best_lds)));
+        }
         if (better) {
             best_eff = eff;
+            best_cost = cost;
             best_conf = conf;
             best_lds = lds;
             best = Tile{TH, TW, ty, tx, lds, mseg};
@@ -210,6 +225,15 @@ bool allow_big_lds(const void *kern) {
 // ---------------------------------------------------------------------------------------
 // conv launch
 // ---------------------------------------------------------------------------------------
+// halo weight of the dgrad (STAGE_ZP2) tile ranking; CISTA_ZP2_HALO_W overrides it (A/B runs)
+double zp2_halo_weight() {
+    static const double w = [] {
+        const char *e = getenv("CISTA_ZP2_HALO_W");
+        return e ? atof(e) : 0.25;
+    }();
+    return w;
+}
+
 template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
@@ -218,7 +242,8 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int NWV = WM * WN, NT = NWV * 64;     // waves, threads per workgroup
     // OCC = waves per SIMD the register budget is sized for (__launch_bounds__): OCC * 4 / NWV
     // workgroups share a CU's LDS
-    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG);
+    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG,
+                         STAGE == STAGE_ZP2 ? zp2_halo_weight() : 0.0);
     if (a.border == 1)          // rows 0 and Hout-1 in 1-row tiles
         t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S), 0};
     else if (a.border == 2)     // columns 0 and Wout-1 in 1-column tiles
