@@ -772,14 +772,25 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
     constexpr int NPXB = MT_W * WM * 16;
     int *ptab = reinterpret_cast<int *>(smem);
     const int n = a.Hin, mw = a.Win, L = 2 * (mw + 2) + 2 * n;
-    // ptab: input pixel index (interior), -(compact border index) - 2 (border line), -1 (outside)
+    // ptab: input pixel index (interior), -(compact border index) - 2 (border line), -1 (outside).
+    // Bit 30 of an interior entry marks input rows 1, n-2 and columns 1, mw-2: fold_fix_kernel
+    // adds their reflected terms and publishes their final |max|, so this epilogue leaves them out
+    // of its own (the partial value would only overestimate the gradient's |max|).  The host keeps
+    // every element offset below 2^31 and the channel count >= 32, so pixel indices stay < 2^26
+    constexpr int FIXB = 1 << 30;
     for (int p = etid; p < NPXB; p += NTH) {
         int v = -1, py, px;
         if (tile_pixel(a, p, py, px)) {
             const int oy = oy0 + py, ox = ox0 + px;
-            if (oy < a.Hout && ox < a.Wout)
-                v = (oy >= 1 && oy <= n && ox >= 1 && ox <= mw) ? (b * n + oy - 1) * mw + ox - 1
-                                                                 : -(b * L + fold_border_index(oy, ox, n, mw)) - 2;
+            if (oy < a.Hout && ox < a.Wout) {
+                if (oy >= 1 && oy <= n && ox >= 1 && ox <= mw) {
+                    const int iy = oy - 1, ix = ox - 1;
+                    const bool fix = iy == 1 || iy == n - 2 || ix == 1 || ix == mw - 2;
+                    v = ((b * n + iy) * mw + ix) | (fix ? FIXB : 0);
+                } else {
+                    v = -(b * L + fold_border_index(oy, ox, n, mw)) - 2;
+                }
+            }
         }
         ptab[p] = v;
     }
@@ -802,7 +813,7 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
     for (int nn = 0; nn < NW; ++nn) bias4[nn] = *(const float4 *)(a.bias + ch0 + 16 * nn);
     auto load_aux = [&](int m, float4 (&A)[NW]) {
         const int off = ptab[(wm * MT_W + m) * 16 + pl];
-        const unsigned o = has_aux ? (unsigned)(off < 0 ? 0 : off) * (unsigned)Cd : 0u;
+        const unsigned o = has_aux ? (unsigned)(off < 0 ? 0 : off & (FIXB - 1)) * (unsigned)Cd : 0u;
 #pragma unroll
         for (int nn = 0; nn < NW; ++nn) A[nn] = *(const float4 *)(abase + o + (has_aux ? 16 * nn : 0));
     };
@@ -816,7 +827,9 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
     for (int m = 0; m < MT_W; ++m) {
         float4 (&cur)[NW] = ring[m % PD];
         asm volatile("" ::: "memory");
-        const int off = ptab[(wm * MT_W + m) * 16 + pl];
+        const int offf = ptab[(wm * MT_W + m) * 16 + pl];
+        const bool pub = offf >= 0 && !(offf & FIXB);           // publishes its |max| here
+        const int off = offf < 0 ? offf : offf & (FIXB - 1);
         float4 rm[NW], r2m[NW];
 #pragma unroll
         for (int nn = 0; nn < NW; ++nn) {
@@ -833,7 +846,7 @@ __device__ __forceinline__ void conv_fold_epilogue(const ConvArgs &a, u32x4 *sme
             }
             rm[nn] = make_float4(r[0], r[1], r[2], r[3]);
             r2m[nn] = make_float4(r2[0], r2[1], r2[2], r2[3]);
-            if (off >= 0) mx = amax4f(mx, rm[nn]);
+            if (pub) mx = amax4f(mx, rm[nn]);
         }
         // refill this ring slot before this m-tile's stores (vmcnt is in order)
         if (m + PD < MT_W) load_aux(m + PD, cur);
