@@ -148,12 +148,32 @@ size_t lds_bytes(int TH, int TW, int S) {
 #define CISTA_MSEG 1      // row-aligned m-tiles for stride-1 convs (0: row-major only, A/B builds)
 #endif
 
-// max_items: staging items (HP rounded to 8, x4 k-groups) one workgroup may hold in registers
-// (0 = unlimited); nbuf: LDS images (2 for the double-buffered loop); seg: row-aligned m-tiles
-// allowed (stride-1 stagings).  Ranking: pixel efficiency (useful / computed pixels) first; at
-// equal efficiency a layout whose m-tile A-fragment reads are bank-conflict free (each m-tile's
-// 16 lanes in one halo row: ds_read_b128 serves 16 lanes of 16 contiguous slots per cycle),
-// then the smaller LDS image.
+// One tile candidate: TW columns, row-major m-tiles (mode 0) or row-aligned m-tile segments
+// (mode 1), as many rows as the workgroup's pixels, the staging registers (max_items: halo
+// items, HP rounded to 8, x4 k-groups, one workgroup may hold; 0 = unlimited) and the LDS
+// (nbuf images, occ workgroups per CU) allow.  False if the width admits no tile.
+bool tile_candidate(int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ, int TW, int mode,
+                    Tile &t, int &conf) {
+    const int mseg = mode ? (TW + 15) / 16 : 0;
+    if (mode && TW % 16 == 0) return false;               // same as row-major
+    int TH = mode ? (block_px / 16) / mseg : block_px / TW;
+    if (TH > Hout) TH = Hout;
+    if (TH < 1) return false;
+    auto items = [&](int th) { return ((((th - 1) * S + 3) * ((TW - 1) * S + 3) + 7) & ~7) * 4; };
+    while (max_items && TH > 1 && items(TH) > max_items) --TH;
+    if (max_items && items(TH) > max_items) return false;
+    const size_t lds = lds_bytes(TH, TW, S) * nbuf;
+    if (lds > 160 * 1024 / (size_t)occ) return false;
+    t = Tile{TH, TW, (Hout + TH - 1) / TH, (Wout + TW - 1) / TW, lds, mseg};
+    // row-major m-tiles that wrap a tile row put two halo rows' slots in one lane group
+    conf = (S == 1 && (mode || TW % 16 == 0)) ? 0 : 1;
+    return true;
+}
+
+// max_items, nbuf, occ: tile_candidate; seg: row-aligned m-tiles allowed (stride-1 stagings).
+// Ranking: pixel efficiency (useful / computed pixels) first; at equal efficiency a layout whose
+// m-tile A-fragment reads are bank-conflict free (each m-tile's 16 lanes in one halo row:
+// ds_read_b128 serves 16 lanes of 16 contiguous slots per cycle), then the smaller LDS image.
 // halo_w > 0: rank by cost per useful output pixel instead, tiles x (block_px + halo_w x halo
 // pixels) x (1 + 0.05 if the m-tile reads are bank-conflicted): the training dgrads (2-chunk K
 // loops at B = 8) otherwise took 48 x 2 tiles (96 px, a 200-pixel halo, conflicted reads) for
@@ -164,46 +184,94 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
     double best_eff = -1.0, best_cost = 1e300;
     int best_conf = 1;
     size_t best_lds = ~(size_t)0;
-    const size_t lds_cap = 160 * 1024 / occ;   // occ workgroups per CU
-    const int mtiles = block_px / 16;
     for (int mode = 0; mode < ((seg && CISTA_MSEG) ? 2 : 1); ++mode)
     for (int TW = 1; TW <= block_px && TW <= Wout; ++TW) {
 #if CISTA_TW16
         // 16-pixel m-tiles that never wrap a tile row read LDS without bank conflicts
         if (Wout >= 16 && (TW % 16) != 0) continue;
 #endif
-        const int mseg = mode ? (TW + 15) / 16 : 0;
-        if (mode && TW % 16 == 0) continue;               // same as row-major
-        int TH = mode ? mtiles / mseg : block_px / TW;
-        if (TH > Hout) TH = Hout;
-        if (TH < 1) continue;
-        auto items = [&](int th) { return ((((th - 1) * S + 3) * ((TW - 1) * S + 3) + 7) & ~7) * 4; };
-        while (max_items && TH > 1 && items(TH) > max_items) --TH;
-        if (max_items && items(TH) > max_items) continue;
-        const size_t lds = lds_bytes(TH, TW, S) * nbuf;
-        if (lds > lds_cap) continue;
-        const int ty = (Hout + TH - 1) / TH, tx = (Wout + TW - 1) / TW;
-        const double eff = (double)Hout * Wout / ((double)ty * tx * block_px);
-        // row-major m-tiles that wrap a tile row put two halo rows' slots in one lane group
-        const int conf = (S == 1 && (mode || TW % 16 == 0)) ? 0 : 1;
+        Tile t;
+        int conf;
+        if (!tile_candidate(Hout, Wout, block_px, S, max_items, nbuf, occ, TW, mode, t, conf)) continue;
+        const double eff = (double)Hout * Wout / ((double)t.ty * t.tx * block_px);
         bool better;
         double cost = 0.0;
         if (halo_w > 0.0) {
-            const double hp = (double)((TH - 1) * S + 3) * ((TW - 1) * S + 3);
-            cost = (double)ty * tx * (block_px + halo_w * hp) * (conf ? 1.05 : 1.0) / ((double)Hout * Wout);
-            better = cost < best_cost - 1e-9 || (cost < best_cost + 1e-9 && lds < best_lds);
+            const double hp = (double)((t.TH - 1) * S + 3) * ((TW - 1) * S + 3);
+            cost = (double)t.ty * t.tx * (block_px + halo_w * hp) * (conf ? 1.05 : 1.0) / ((double)Hout * Wout);
+            better = cost < best_cost - 1e-9 || (cost < best_cost + 1e-9 && t.lds < best_lds);
         } else {
             better = eff > best_eff + 1e-9 ||
-                     (eff > best_eff - 1e-9 && (conf < best_conf || (conf == best_conf && lds < best_lds)));
+                     (eff > best_eff - 1e-9 && (conf < best_conf || (conf == best_conf && t.lds < best_lds)));
         }
         if (better) {
             best_eff = eff;
             best_cost = cost;
             best_conf = conf;
-            best_lds = lds;
-            best = Tile{TH, TW, ty, tx, lds, mseg};
+            best_lds = t.lds;
+            best = t;
         }
     }
+    return best;
+}
+
+// Two-region tiling.  No rectangle of a 192-pixel workgroup tiles 90 x 120 exactly (the best,
+// 6 x 32 or 6 x 30 in row segments, computes 0.9375 useful pixels per slot: every row of tiles
+// ends in a partly idle tile).  Columns [0, wa) are cut into an exact multiple of one tile width
+// (region a) and the strip [wa, Wout) gets its own tile shape (region b), launched separately:
+// 45 + 12 = 57 tiles per 90 x 120 image instead of 60 (0.987; the 96-pixel convs 113 instead of
+// 115, and 90 of those 113 tiles read LDS conflict-free).  Only for forward launches with enough
+// workgroups (at B = 1 the second launch costs more latency than its slots save); memoised.
+#ifndef CISTA_SPLIT
+#define CISTA_SPLIT 1
+#endif
+struct TilePlan { Tile a, b; int wa; };   // b.tx == 0: one region (a covers every column)
+
+TilePlan plan_tiles(int B, int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ, bool seg,
+                    double halo_w) {
+    TilePlan best{choose_tile(Hout, Wout, block_px, S, max_items, nbuf, occ, seg, halo_w), Tile{}, Wout};
+    if (!CISTA_SPLIT || halo_w > 0.0 || (long)B * best.a.ty * best.a.tx < 2048) return best;
+    struct Key { int Hout, Wout, block_px, S, max_items, nbuf, occ, seg; };
+    struct Ent { Key k; TilePlan p; };
+    static std::mutex mu;
+    static Ent cache[64];
+    static int ncache = 0;
+    const Key key{Hout, Wout, block_px, S, max_items, nbuf, occ, seg ? 1 : 0};
+    {
+        std::lock_guard<std::mutex> lock(mu);
+        for (int i = 0; i < ncache; ++i)
+            if (!memcmp(&cache[i].k, &key, sizeof(Key))) return cache[i].p;
+    }
+    // ranked by tiles per image, then by tiles whose m-tile reads are bank-conflicted (weighting
+    // those 1.05, as the dgrad ranking does, kept the 192-pixel convs at one region: 8410 / 8376
+    // frames/s against 8566 / 8541 unweighted, same box)
+    long best_tiles = (long)best.a.ty * best.a.tx, best_conf = 0;
+    {
+        Tile t;
+        int conf = 0;
+        if (tile_candidate(Hout, Wout, block_px, S, max_items, nbuf, occ, best.a.TW, best.a.mseg ? 1 : 0, t, conf))
+            best_conf = conf ? best_tiles : 0;
+    }
+    for (int mode = 0; mode < ((seg && CISTA_MSEG) ? 2 : 1); ++mode)
+        for (int TW = 1; TW <= block_px && TW < Wout; ++TW) {
+            const int wa = (Wout / TW) * TW;
+            if (wa == Wout) continue;
+            Tile ta, tb;
+            int ca, cb;
+            if (!tile_candidate(Hout, wa, block_px, S, max_items, nbuf, occ, TW, mode, ta, ca)) continue;
+            tb = choose_tile(Hout, Wout - wa, block_px, S, max_items, nbuf, occ, seg, 0.0);
+            if (!tile_candidate(Hout, Wout - wa, block_px, S, max_items, nbuf, occ, tb.TW, tb.mseg ? 1 : 0, tb, cb))
+                continue;
+            const long tiles = (long)ta.ty * ta.tx + (long)tb.ty * tb.tx;
+            const long conf = (ca ? (long)ta.ty * ta.tx : 0) + (cb ? (long)tb.ty * tb.tx : 0);
+            if (tiles < best_tiles || (tiles == best_tiles && conf < best_conf)) {
+                best_tiles = tiles;
+                best_conf = conf;
+                best = TilePlan{ta, tb, wa};
+            }
+        }
+    std::lock_guard<std::mutex> lock(mu);
+    if (ncache < 64) cache[ncache++] = Ent{key, best};
     return best;
 }
 
@@ -242,21 +310,16 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int NWV = WM * WN, NT = NWV * 64;     // waves, threads per workgroup
     // OCC = waves per SIMD the register budget is sized for (__launch_bounds__): OCC * 4 / NWV
     // workgroups share a CU's LDS
-    Tile t = choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG,
-                         STAGE == STAGE_ZP2 ? zp2_halo_weight() : 0.0);
+    constexpr bool SPLIT_OK = (STAGE == STAGE_S1 || STAGE == STAGE_S2D) && EPI != EPI_FOLD;
+    TilePlan plan{choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG,
+                              STAGE == STAGE_ZP2 ? zp2_halo_weight() : 0.0),
+                  Tile{}, a.Wout};
+    if (SPLIT_OK && a.border == 0)
+        plan = plan_tiles(a.B, a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG, 0.0);
     if (a.border == 1)          // rows 0 and Hout-1 in 1-row tiles
-        t = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S), 0};
+        plan.a = Tile{1, block_px, 2, (a.Wout + block_px - 1) / block_px, lds_bytes(1, block_px, S), 0};
     else if (a.border == 2)     // columns 0 and Wout-1 in 1-column tiles
-        t = Tile{block_px, 1, (a.Hout + block_px - 1) / block_px, 2, lds_bytes(block_px, 1, S), 0};
-    a.TH = t.TH;
-    a.TW = t.TW;
-    a.pitch = t.mseg ? 16 * t.mseg : t.TW;
-    a.rcp_pitch = 1.0f / (float)a.pitch;
-    // small_div's range: halo pixels < 2048, pitch and halo width <= 512
-    if (((t.TH - 1) * S + 3) * ((t.TW - 1) * S + 3) >= 2048 || a.pitch > 512 || (t.TW - 1) * S + 3 > 512)
-        return CISTA_ERR_UNSUPPORTED;
-    a.tiles_y = t.ty;
-    a.tiles_x = t.tx;
+        plan.a = Tile{block_px, 1, (a.Hout + block_px - 1) / block_px, 2, lds_bytes(block_px, 1, S), 0};
     constexpr int nblk_cols = WN * NW * 16;
     if (a.N % nblk_cols) return CISTA_ERR_UNSUPPORTED;
     // the training variant (SV) only for epilogues that save activations, and only when asked
@@ -266,11 +329,6 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
         if ((EPI == EPI_LSTM ? a.out2 : a.out1) != nullptr)
             kern = conv3x3_split3<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, true, OCC>;
     if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
-#if CISTA_XCD
-    dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
-#else
-    dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
-#endif
     // the epilogue indexes outputs with 32-bit element offsets (pixel * Cout, x4 for out2)
     // and the double-buffered staging reads inputs with 32-bit element offsets
     if ((long long)a.B * a.Hout * a.Wout * a.Cout * (a.out2 || EPI == EPI_PH4 ? 4 : 1) >= (1LL << 31))
@@ -285,9 +343,29 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
-    hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
-    return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+    // one launch per tile region (plan_tiles): region b's tiles start at column wa
+    for (int r = 0; r < (plan.b.tx ? 2 : 1); ++r) {
+        const Tile t = r ? plan.b : plan.a;
+        a.ox_base = r ? plan.wa : 0;
+        a.TH = t.TH;
+        a.TW = t.TW;
+        a.pitch = t.mseg ? 16 * t.mseg : t.TW;
+        a.rcp_pitch = 1.0f / (float)a.pitch;
+        // small_div's range: halo pixels < 2048, pitch and halo width <= 512
+        if (((t.TH - 1) * S + 3) * ((t.TW - 1) * S + 3) >= 2048 || a.pitch > 512 || (t.TW - 1) * S + 3 > 512)
+            return CISTA_ERR_UNSUPPORTED;
+        a.tiles_y = t.ty;
+        a.tiles_x = t.tx;
+#if CISTA_XCD
+        dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
+#else
+        dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
+#endif
+        const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
+        hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
+        if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
+    }
+    return CISTA_OK;
 }
 
 // pick the wave tiling from the number of packed output columns.

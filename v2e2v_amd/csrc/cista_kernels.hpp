@@ -175,6 +175,7 @@ struct ConvArgs {
     int fsplit;
     float *fborder;
     unsigned probe_mask; // EPI_ISTA_P_L2 only
+    int ox_base;         // first output column of this launch's tiles (two-region tilings)
 };
 
 // floor(n / d) for 0 <= n < 2048 and 1 <= d <= 512 through fp32, given rcp_d = 1 / d correctly
@@ -894,7 +895,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
     // 0 and Hout-1 (1), or 1-column tiles on columns 0 and Wout-1 (2) -- the phase-decomposed
     // upsample's exact border pass.  Compiled into STAGE_UP kernels alone: in the others the
     // runtime select cost 9 VGPRs and spilled the 247-VGPR ISTA convs.
-    int oy0 = ty * a.TH, ox0 = tx * a.TW;
+    int oy0 = ty * a.TH, ox0 = a.ox_base + tx * a.TW;
     if constexpr (STAGE == STAGE_UP) {
         if (a.border == 1) oy0 = ty ? a.Hout - 1 : 0;
         if (a.border == 2) ox0 = tx ? a.Wout - 1 : 0;
