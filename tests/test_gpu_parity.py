@@ -330,6 +330,30 @@ def test_batch48_equals_single():
             assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
 
 
+@pytest.mark.parametrize("H,W,B", [(120, 180, 72), (90, 120, 140)])
+def test_two_region_tiling_equals_single(H, W, B):
+    """Two-region conv tiling (plan_tiles, cista_abi.hip): at these batches the forward convs
+    of the 60 x 90 / 45 x 60 internal grids run as an exact-width region plus a 10- / 12-column
+    strip launch (192- and 96-pixel workgroups), while a B=1 run keeps one region.  Every checked
+    sample of the batched frame equals its own B=1 run bit for bit (same per-pixel arithmetic,
+    different tiles), and one matches the oracle."""
+    params = fx.stress_params(64, 2, 5, seed=H)
+    m = make_model(depth=2, params=params)
+    rng = np.random.default_rng(W)
+    vox = rng.standard_normal((B, 5, H, W)).astype(np.float32)
+    prev = rng.random((B, 1, H, W)).astype(np.float32)
+    with torch.no_grad():
+        r, s = m(gpu(vox), gpu(prev), None)
+        for i in (0, B // 2 + 1, B - 1):
+            ri, si = m(gpu(vox[i:i + 1]), gpu(prev[i:i + 1]), None)
+            assert torch.equal(r[i:i + 1], ri), i
+            assert torch.equal(s[0][i:i + 1], si[0]) and torch.equal(s[1][i:i + 1], si[1]), i
+            assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
+    o_rec, o_st = CistaLSTCOracle(params, 2).forward(vox[B - 1:B], prev[B - 1:B], None)
+    assert elem_rel_err(r[B - 1:B].cpu().numpy(), o_rec) < TOL
+    assert rel_err(s[1][B - 1:B].cpu().numpy(), o_st[1]) < TOL
+
+
 def test_determinism_and_batch_independence():
     """Size-independent properties at the bench size: bit-identical re-runs, and sample i of a
     batched launch equals the same sample run alone (no cross-sample coupling)."""
