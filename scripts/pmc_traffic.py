@@ -5,6 +5,11 @@ wide (16 B/lane) coalesced read, which is what every staging / epilogue read of 
 is, so read bytes = 2 * FETCH_SIZE; WRITE_SIZE is exact for 16 B/lane stores.  Both counters
 are in KiB and were collected in separate passes (they cannot share the 4 TCC slots).
 
+A layer may run as several dispatches of one kernel (the two-region tiling of plan_tiles: an
+exact-width region and a column strip, different grid sizes): the counters and durations are
+averaged per (layer, grid size) and summed over the grid sizes, i.e. reported per layer
+launch (what bench.py times with HIP events).
+
 usage: python scripts/pmc_traffic.py 'gpurun_out/pmcl_*/run_counter_collection.csv' out.json [lib.so]
 The library's sha256 is recorded: bench.py only quotes the traffic for the build it measured.
 """
@@ -47,6 +52,7 @@ def lib_sha256(path):
 
 
 def main(pattern, out, lib=None):
+    # (layer, grid size) -> counter -> values; (layer, grid size) -> durations (us)
     vals = collections.defaultdict(lambda: collections.defaultdict(list))
     durs = collections.defaultdict(list)
     names = {}
@@ -56,16 +62,20 @@ def main(pattern, out, lib=None):
             if layer is None:
                 continue
             names[layer] = kname
-            vals[layer][r["Counter_Name"]].append(float(r["Counter_Value"]))
-            durs[layer].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+            key = (layer, int(r.get("Grid_Size", 0) or 0))
+            vals[key][r["Counter_Name"]].append(float(r["Counter_Value"]))
+            durs[key].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
+    mean = lambda v: sum(v) / len(v)
     res = {}
-    for layer, d in vals.items():
-        if "FETCH_SIZE" not in d or "WRITE_SIZE" not in d:
+    for layer in sorted({k[0] for k in vals}):
+        keys = sorted(k for k in vals if k[0] == layer)
+        if any("FETCH_SIZE" not in vals[k] or "WRITE_SIZE" not in vals[k] for k in keys):
             continue
-        fk = sum(d["FETCH_SIZE"]) / len(d["FETCH_SIZE"])
-        wk = sum(d["WRITE_SIZE"]) / len(d["WRITE_SIZE"])
-        res[layer] = {"kernel": names[layer], "dispatches": len(d["FETCH_SIZE"]),
-                      "mean_dur_us_profiled": round(sum(durs[layer]) / len(durs[layer]), 2),
+        fk = sum(mean(vals[k]["FETCH_SIZE"]) for k in keys)
+        wk = sum(mean(vals[k]["WRITE_SIZE"]) for k in keys)
+        res[layer] = {"kernel": names[layer], "dispatches": sum(len(vals[k]["FETCH_SIZE"]) for k in keys),
+                      "grids_per_launch": [k[1] for k in keys],
+                      "mean_dur_us_profiled": round(sum(mean(durs[k]) for k in keys), 2),
                       "FETCH_SIZE_KiB": round(fk, 1), "WRITE_SIZE_KiB": round(wk, 1),
                       "hbm_bytes_per_launch": round((2 * fk + wk) * 1024)}
     lib = lib or os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "v2e2v_amd",

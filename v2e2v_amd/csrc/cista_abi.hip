@@ -218,10 +218,11 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
 // Two-region tiling.  No rectangle of a 192-pixel workgroup tiles 90 x 120 exactly (the best,
 // 6 x 32 or 6 x 30 in row segments, computes 0.9375 useful pixels per slot: every row of tiles
 // ends in a partly idle tile).  Columns [0, wa) are cut into an exact multiple of one tile width
-// (region a) and the strip [wa, Wout) gets its own tile shape (region b), launched separately:
-// 45 + 12 = 57 tiles per 90 x 120 image instead of 60 (0.987; the 96-pixel convs 113 instead of
-// 115, and 90 of those 113 tiles read LDS conflict-free).  Only for forward launches with enough
-// workgroups (at B = 1 the second launch costs more latency than its slots save); memoised.
+// (region a) and the strip [wa, Wout) gets its own tile shape (region b); both run in one launch,
+// region b's items after region a's: 54 + 3 = 57 tiles per 90 x 120 image instead of 60 (0.987),
+// the 96-pixel convs 105 + 8 = 113 instead of 115.  Only where the launch is at least two
+// dispatch rounds (B x tiles >= 1024 items on 512 workgroup slots): a one-round launch takes one
+// workgroup lifetime whatever its item count.  Memoised per shape.
 #ifndef CISTA_SPLIT
 #define CISTA_SPLIT 1
 #endif
@@ -230,7 +231,7 @@ struct TilePlan { Tile a, b; int wa; };   // b.tx == 0: one region (a covers eve
 TilePlan plan_tiles(int B, int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ, bool seg,
                     double halo_w) {
     TilePlan best{choose_tile(Hout, Wout, block_px, S, max_items, nbuf, occ, seg, halo_w), Tile{}, Wout};
-    if (!CISTA_SPLIT || halo_w > 0.0 || (long)B * best.a.ty * best.a.tx < 2048) return best;
+    if (!CISTA_SPLIT || halo_w > 0.0 || (long)B * best.a.ty * best.a.tx < 1024) return best;
     struct Key { int Hout, Wout, block_px, S, max_items, nbuf, occ, seg; };
     struct Ent { Key k; TilePlan p; };
     static std::mutex mu;
@@ -310,7 +311,8 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int NWV = WM * WN, NT = NWV * 64;     // waves, threads per workgroup
     // OCC = waves per SIMD the register budget is sized for (__launch_bounds__): OCC * 4 / NWV
     // workgroups share a CU's LDS
-    constexpr bool SPLIT_OK = (STAGE == STAGE_S1 || STAGE == STAGE_S2D) && EPI != EPI_FOLD;
+    constexpr bool SPLIT_OK = (STAGE == STAGE_S1 || STAGE == STAGE_S2D || STAGE == STAGE_UP || STAGE == STAGE_CLAMP) &&
+                              EPI != EPI_FOLD;
     TilePlan plan{choose_tile(a.Hout, a.Wout, block_px, S, NI ? NI * NT : 0, NI ? 2 : 1, OCC * 4 / NWV, SEG,
                               STAGE == STAGE_ZP2 ? zp2_halo_weight() : 0.0),
                   Tile{}, a.Wout};
@@ -343,28 +345,37 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     // + 3 x NWV words of range-pass scratch (overflow bits, max, min) right after the epilogue's
     // LDS (inside the dead staging images when those are larger)
     a.lds_flag = (int)(epi_lds / 4);
-    // one launch per tile region (plan_tiles): region b's tiles start at column wa
-    for (int r = 0; r < (plan.b.tx ? 2 : 1); ++r) {
-        const Tile t = r ? plan.b : plan.a;
-        a.ox_base = r ? plan.wa : 0;
-        a.TH = t.TH;
-        a.TW = t.TW;
-        a.pitch = t.mseg ? 16 * t.mseg : t.TW;
-        a.rcp_pitch = 1.0f / (float)a.pitch;
+    // one launch; region b's items (plan_tiles: columns [wa, Wout)) follow region a's
+    auto geom_ok = [&](const Tile &t) {
         // small_div's range: halo pixels < 2048, pitch and halo width <= 512
-        if (((t.TH - 1) * S + 3) * ((t.TW - 1) * S + 3) >= 2048 || a.pitch > 512 || (t.TW - 1) * S + 3 > 512)
-            return CISTA_ERR_UNSUPPORTED;
-        a.tiles_y = t.ty;
-        a.tiles_x = t.tx;
+        const int pitch = t.mseg ? 16 * t.mseg : t.TW;
+        return ((t.TH - 1) * S + 3) * ((t.TW - 1) * S + 3) < 2048 && pitch <= 512 && (t.TW - 1) * S + 3 <= 512;
+    };
+    if (!geom_ok(plan.a) || (plan.b.tx && !geom_ok(plan.b))) return CISTA_ERR_UNSUPPORTED;
+    a.ox_base = 0;
+    a.TH = plan.a.TH;
+    a.TW = plan.a.TW;
+    a.pitch = plan.a.mseg ? 16 * plan.a.mseg : plan.a.TW;
+    a.rcp_pitch = 1.0f / (float)a.pitch;
+    a.tiles_y = plan.a.ty;
+    a.tiles_x = plan.a.tx;
+    a.tiles_x_b = plan.b.tx;               // 0: one region
+    a.tiles_y_b = plan.b.ty;
+    a.TH_b = plan.b.TH;
+    a.TW_b = plan.b.TW;
+    a.pitch_b = plan.b.mseg ? 16 * plan.b.mseg : plan.b.TW;
+    a.rcp_pitch_b = plan.b.tx ? 1.0f / (float)a.pitch_b : 0.0f;
+    a.wa = plan.wa;
+    const long tiles = (long)plan.a.ty * plan.a.tx + (long)plan.b.ty * plan.b.tx;
 #if CISTA_XCD
-        dim3 grid((unsigned)((long)a.B * t.ty * t.tx * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
+    dim3 grid((unsigned)((long)a.B * tiles * (a.N / nblk_cols)));   // 1-D, XCD-aware order in the kernel
 #else
-        dim3 grid((unsigned)((long)a.B * t.ty * t.tx), (unsigned)(a.N / nblk_cols));
+    dim3 grid((unsigned)((long)a.B * tiles), (unsigned)(a.N / nblk_cols));
 #endif
-        const size_t lds = t.lds > epi_lds + 12 * NWV ? t.lds : epi_lds + 12 * NWV;
-        hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
-        if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
-    }
+    const size_t tlds = plan.b.lds > plan.a.lds ? plan.b.lds : plan.a.lds;
+    const size_t lds = tlds > epi_lds + 12 * NWV ? tlds : epi_lds + 12 * NWV;
+    hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
+    if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     return CISTA_OK;
 }
 

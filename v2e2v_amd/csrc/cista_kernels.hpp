@@ -175,7 +175,12 @@ struct ConvArgs {
     int fsplit;
     float *fborder;
     unsigned probe_mask; // EPI_ISTA_P_L2 only
-    int ox_base;         // first output column of this launch's tiles (two-region tilings)
+    // two-region tilings (plan_tiles): the tile items of region a (columns [0, wa), the fields
+    // above) come first, then those of region b (columns [wa, Wout), geometry below; nb_tiles 0:
+    // one region).  ox_base: the first output column of the region being run (set per item)
+    int ox_base;
+    int TH_b, TW_b, tiles_x_b, tiles_y_b, pitch_b, wa;
+    float rcp_pitch_b;
 };
 
 // floor(n / d) for 0 <= n < 2048 and 1 <= d <= 512 through fp32, given rcp_d = 1 / d correctly
@@ -1481,7 +1486,21 @@ __global__ __launch_bounds__(WM * WN * 64, OCC) void conv3x3_split3(const ConvAr
 #else
     const unsigned witem = blockIdx.x;
 #endif
-    conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV>(a, smem, witem);
+    // region b of a two-region tiling: its items follow region a's, with their own geometry
+    const unsigned items_a = (unsigned)a.B * (unsigned)(a.tiles_y * a.tiles_x) *
+#if CISTA_XCD
+                             ((unsigned)a.N / (unsigned)(WN * NW * 16));
+#else
+                             1u;
+#endif
+    ConvArgs ar = a;
+    unsigned w = witem;
+    if (a.tiles_x_b && witem >= items_a) {      // workgroup-uniform
+        ar.TH = a.TH_b; ar.TW = a.TW_b; ar.tiles_x = a.tiles_x_b; ar.tiles_y = a.tiles_y_b;
+        ar.pitch = a.pitch_b; ar.rcp_pitch = a.rcp_pitch_b; ar.ox_base = a.wa;
+        w -= items_a;
+    }
+    conv_tile<MT_W, NW, WM, WN, STAGE, EPI, G, PF, NI, SV>(ar, smem, w);
 }
 
 // ------------------------------------------------------------------------------------------
