@@ -74,6 +74,9 @@ def parse():
                    help="recurrent frames per CPU-baseline sequence (B=1); sequences repeat to ~10 s")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--layer-reps", type=int, default=10)
+    p.add_argument("--adam", choices=["fused", "foreach"], default="fused",
+                   help="--mode train: torch.optim.Adam implementation (the same update; fused = one "
+                        "multi-tensor kernel per step instead of a chain of foreach launches)")
     p.add_argument("--mode", choices=["infer", "train", "v2e2v"], default="infer",
                    help="infer: the headline metric (config c2); train: BPTT step (configs c3/c4); "
                         "v2e2v: emulator + reconstruction at 720x1280 (config c5)")
@@ -274,7 +277,7 @@ def train_main(args, torch, vd, rank, world, device):
         # under torchrun (any N, N=1 included): one bucketed RCCL all-reduce of the gradients
         net = torch.nn.parallel.DistributedDataParallel(model, device_ids=[device.index],
                                                         broadcast_buffers=False)
-    opt = torch.optim.Adam(model.parameters(), lr=1e-4)
+    opt = torch.optim.Adam(model.parameters(), lr=1e-4, **({"fused": True} if args.adam == "fused" else {}))
     vox = synth_voxels(torch, L, B, nb, H, W, args.num_events, seed=2000 + rank, device=device)
     target = torch.rand(B, 1, H, W, device=device, generator=torch.Generator(device=device).manual_seed(3))
 
@@ -325,7 +328,8 @@ def train_main(args, torch, vd, rank, world, device):
             "config": {"workload": f"train_e2v BPTT len {L}, batch {B}/GPU, {H}x{W}",
                        "batch_per_gpu": B, "global_batch": B * world, "len_sequence": L,
                        "parallelism": f"ddp{world}" if vd.active() else "single",
-                       "process_group": (torch.distributed.get_backend() if vd.active() else None)},
+                       "process_group": (torch.distributed.get_backend() if vd.active() else None),
+                       "optimizer": f"torch.optim.Adam lr 1e-4 ({args.adam})"},
             "loss": float(loss.item()),
             "roofline": roofline, "cpu_baseline": cpu,
             "peak_mem_gb": round(torch.cuda.max_memory_allocated(device) / 1e9, 2)}), flush=True)
