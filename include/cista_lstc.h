@@ -185,6 +185,15 @@ int cista_layer_fused(const cista_config *cfg, int layer);
 int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, int B, int H,
                        int W, const cista_frame_io *io, void *workspace, size_t workspace_bytes,
                        void *stream);
+/* the tiling of a forward conv's throughput launch over a Hout x Wout output (stride 1,
+ * block_px = 192 or 96 pixels per workgroup, B samples): region a = ty x tx tiles of TH x TW
+ * pixels over columns [0, wa), region b (tx == 0: none) over columns [wa, Wout) -- the two-region
+ * tiling of cista_abi.hip plan_tiles, both regions in one launch.  out[14] = {TH, TW, ty, tx,
+ * mseg} of region a, the same of region b, wa, the tile count and mseg of the best one-region
+ * tiling, 0; mseg > 0: each tile row is mseg 16-pixel m-tiles (row-aligned, conflict-free LDS
+ * reads), 0: row-major m-tiles.  Host-only (no device call); introspection for tests, not a
+ * reference interface. */
+int cista_tile_plan(int B, int Hout, int Wout, int block_px, int *out);
 
 /* ---- training: BPTT backward (reference train_e2v.py:108-130
  * differentiates through the whole recurrent sequence with autograd) ----

@@ -109,3 +109,42 @@ def test_voxelizer_surface_cpu():
     assert L.cista_voxelize(None, None, 1, 0, 5, 8, 8, 7, 0.0, None, None, 0, None) == 1
     assert L.cista_voxel_preprocess(None, 1, 5, 8, 8, 3, 0.0, None, 0, None) == 1
     assert L.cista_voxelize(None, None, 0, 0, 5, 8, 8, 0, 0.0, None, None, 0, None) == 0   # B == 0: no-op
+
+
+@pytest.mark.parametrize("block_px", [192, 96])
+def test_two_region_tile_plan_invariants(block_px):
+    """The forward convs' tiling (cista_tile_plan -> plan_tiles, host-only): over many output
+    shapes the plan covers every row and column once (region a an exact multiple of its tile
+    width, region b the remaining strip), never computes more tiles than the best one-region
+    tiling, keeps each tile inside the workgroup's pixels and its halo inside the staging
+    registers (4 items x 256 threads) and two LDS images per CU half; at 90 x 120 it cuts the
+    192-pixel tiles from 60 to 57 and the 96-pixel ones from 115 to 113; and a
+    launch of fewer than 1024 items keeps one region."""
+    L = _lib.lib()
+    rng = np.random.default_rng(block_px)
+    shapes = [(90, 120), (60, 90), (45, 60), (360, 640), (1, 7), (7, 1), (16, 16), (33, 200)]
+    shapes += [tuple(int(v) for v in rng.integers(1, 260, 2)) for _ in range(120)]
+    out = (ctypes.c_int * 14)()
+    for H, W in shapes:
+        assert L.cista_tile_plan(256, H, W, block_px, out) == 0
+        THa, TWa, tya, txa, msa, THb, TWb, tyb, txb, msb, wa, one, _, _ = list(out)
+        for TH, TW, ty, tx, ms in ((THa, TWa, tya, txa, msa), (THb, TWb, tyb, txb, msb)):
+            if tx == 0:
+                continue
+            assert ty * TH >= H and (ty - 1) * TH < H
+            slots = TH * (16 * ms if ms else TW)
+            assert TW >= 1 and slots <= block_px, (H, W, TH, TW, ms)
+            halo = (TH + 2) * (TW + 2)
+            assert ((halo + 7) & ~7) * 4 <= 4 * 256 and ((halo + 15) & ~15) * 128 * 2 <= 80 * 1024
+        if txb == 0:
+            assert wa == W and (txa - 1) * TWa < W <= txa * TWa
+        else:
+            assert 0 < wa < W and txa * TWa == wa
+            assert (txb - 1) * TWb < W - wa <= txb * TWb
+        assert tya * txa + tyb * txb <= one, (H, W)
+    assert L.cista_tile_plan(256, 90, 120, block_px, out) == 0
+    assert out[2] * out[3] + out[7] * out[8] == {192: 57, 96: 113}[block_px]
+    assert out[11] == {192: 60, 96: 115}[block_px]
+    assert L.cista_tile_plan(1, 90, 120, block_px, out) == 0          # 60 / 115 items: one round
+    assert out[8] == 0 and out[10] == 120
+    assert L.cista_tile_plan(256, 90, 120, 100, out) != 0

@@ -1860,6 +1860,24 @@ double cista_layer_macs(const cista_config *cfg, int layer, int B, int H, int W)
     return layer_macs(*cfg, layer, B, H, W);
 }
 
+int cista_tile_plan(int B, int Hout, int Wout, int block_px, int *out) {
+    if (!out || B < 1 || Hout < 1 || Wout < 1 || (block_px != 192 && block_px != 96)) return CISTA_ERR_INVALID;
+    // the forward double-buffered configurations: NI = 4 halo items per thread x 256 threads,
+    // two LDS images, two workgroups per CU, row-aligned m-tiles allowed (launch_conv_cfg)
+    const TilePlan p = plan_tiles(B, Hout, Wout, block_px, 1, 4 * 256, 2, 2, true, 0.0);
+    const Tile *t[2] = {&p.a, &p.b};
+    for (int r = 0; r < 2; ++r) {
+        out[5 * r + 0] = t[r]->TH; out[5 * r + 1] = t[r]->TW; out[5 * r + 2] = t[r]->ty;
+        out[5 * r + 3] = t[r]->tx; out[5 * r + 4] = t[r]->mseg;
+    }
+    out[10] = p.wa;
+    const Tile one = choose_tile(Hout, Wout, block_px, 1, 4 * 256, 2, 2, true, 0.0);
+    out[11] = one.ty * one.tx;
+    out[12] = one.mseg;
+    out[13] = 0;
+    return CISTA_OK;
+}
+
 int cista_layer_fused(const cista_config *cfg, int layer) {
     if (!cfg_ok(cfg)) return 0;
     return layer == CISTA_LAYER_W0 && fused_input(*cfg) ? 1 : 0;
