@@ -392,3 +392,37 @@ def test_small_images_bptt_against_fp64_autograd(H, W, C, NB):
         if not e < GTOL:
             bad[k] = e
     assert not bad, bad
+
+
+def test_training_two_region_tiling_equals_single():
+    """Training at a batch whose forward convs take the two-region tiling (B=40 at 180x240:
+    2400 items for the 192-pixel convs, past plan_tiles' 1024) while B=1 keeps one region: the
+    training forward's frame and states of every checked sample equal its own B=1 training run
+    bit for bit; the events / previous-image gradients of one backward (fed by the saved
+    activations the split-tile SV kernels wrote) agree within 1e-5 of their max: the backward's
+    fp16 gradient splits take one power-of-two scale per batch tensor, so a sample's small
+    values meet the fp16 subnormals at a different point in a batch than alone (last bits)."""
+    B = 40
+    m = CistaLSTCNet([180, 240], base_channels=64, depth=5, num_bins=5)
+    params = fx.stress_params(64, 5, 5, seed=41, lam=0.05)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, 5)
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    rng = np.random.default_rng(5)
+    vox = rng.standard_normal((B, 5, 180, 240)).astype(np.float32)
+    prev = rng.random((B, 1, 180, 240)).astype(np.float32)
+    ev, pi = gpu(vox, True), gpu(prev, True)
+    r, s = m(ev, pi, None)
+    (r.sum() + s[1].square().mean()).backward()
+    for i in (0, 23, B - 1):
+        evi, pii = gpu(vox[i:i + 1], True), gpu(prev[i:i + 1], True)
+        ri, si = m(evi, pii, None)
+        assert torch.equal(r[i:i + 1].detach(), ri.detach()), i
+        assert torch.equal(s[1][i:i + 1].detach(), si[1].detach()), i
+        assert torch.equal(s[2][1][i:i + 1].detach(), si[2][1].detach()), i
+        # the state term's mean over B (vs over 1) scales its gradient by 1 / B: use the same loss
+        (ri.sum() + si[1].square().sum() / s[1].numel()).backward()
+        e1, e2 = rel_err(ev.grad[i:i + 1].cpu().numpy(), evi.grad.cpu().numpy()), \
+            rel_err(pi.grad[i:i + 1].cpu().numpy(), pii.grad.cpu().numpy())
+        print(f"sample {i}: events grad {e1:.2e}, prev-image grad {e2:.2e}")
+        assert e1 < 1e-5 and e2 < 1e-5, (i, e1, e2)
