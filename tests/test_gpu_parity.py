@@ -330,11 +330,13 @@ def test_batch48_equals_single():
             assert torch.equal(s[2][0][i:i + 1], si[2][0]) and torch.equal(s[2][1][i:i + 1], si[2][1]), i
 
 
-@pytest.mark.parametrize("H,W,B", [(120, 180, 72), (90, 120, 140)])
+@pytest.mark.parametrize("H,W,B", [(120, 180, 72), (90, 120, 140), (128, 194, 32), (74, 166, 60)])
 def test_two_region_tiling_equals_single(H, W, B):
     """Two-region conv tiling (plan_tiles, cista_abi.hip): at these batches the forward convs
-    of the 60 x 90 / 45 x 60 internal grids run as an exact-width region plus a 10- / 12-column
-    strip launch (192- and 96-pixel workgroups), while a B=1 run keeps one region.  Every checked
+    of the 60 x 90 / 45 x 60 / 64 x 97 / 37 x 83 internal grids run as an exact-width region
+    plus a column strip (10 / 12 columns; at 64 x 97 a 1-column strip of 64 x 1 tiles, at
+    37 x 83 strips of 37 x 3 and 19 x 5 tiles) in the same launch, while a B=1 run keeps one
+    region.  Every checked
     sample of the batched frame equals its own B=1 run bit for bit (same per-pixel arithmetic,
     different tiles), and one matches the oracle."""
     params = fx.stress_params(64, 2, 5, seed=H)
