@@ -46,7 +46,13 @@ def parse():
     -c/--base_channels, -s/--len_sequence, --batch_size, --num_events, --num_pack_frames);
     the older spellings stay as aliases."""
     p = argparse.ArgumentParser(description=__doc__.split("\n")[0])
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (= ranks) to measure; without a rank launcher, N > 1 starts N child ranks "
+                        "itself (launch_ranks); under torchrun it must equal WORLD_SIZE (default: "
+                        "WORLD_SIZE, else 1)")
+    p.add_argument("--dry-run", action="store_true",
+                   help="launcher check without a GPU: the ranks come up over gloo, time a trivial CPU "
+                        "step and rank 0 prints the JSON line (n_gpus, ranks_seen); no HIP call")
     p.add_argument("--steps", type=int, default=3)
     p.add_argument("--warmup", type=int, default=1)
     # 256 sequences x 15 frames of 180x240 state and voxels are ~4 GB of the 288 GB HBM; the tiles
@@ -185,7 +191,7 @@ def v2e2v_main(args, torch, vd, rank, world, device):
     if rank == 0:
         print(json.dumps({
             "metric": "V2E2V reconstructed frames/sec (v2e emulator + CISTA-LSTC) at 720x1280",
-            "value": round(frames_done / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "value": round(frames_done / elapsed, 2), "unit": "frames/s", "n_gpus": world, **pg_info(vd),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -320,7 +326,7 @@ def train_main(args, torch, vd, rank, world, device):
     if rank == 0:
         print(json.dumps({
             "metric": "BPTT training frames/sec at 180x240 5-bin depth=5 (len_sequence 15)",
-            "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world,
+            "value": round(frames / elapsed, 2), "unit": "frames/s", "n_gpus": world, **pg_info(vd),
             "steps": args.steps, "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 2), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": None, "dtype": "f32",
@@ -574,6 +580,9 @@ def dominant_roofline(layers, lib_mod, traffic_tag=None):
     roofline = dict(bound="mfma", achieved=round(dom["tflops"], 2), peak=round(peak, 1),
                     unit="TFLOP/s", frac=round(dom["tflops"] / peak, 4), traffic=None,
                     kernel=dom_name, launch_ms=round(dom["ms"], 4),
+                    kernel_rule="the layer with the largest HIP-event ms x launches per frame; ISTA D and "
+                                "ISTA P are twins (same MACs, 5 launches each, times within ~3 %), and "
+                                "rocprof's per-dispatch means may rank the other one first",
                     flop_per_launch=2 * dom["macs"],
                     note="achieved = algorithmic fp32 FLOPs (2 x MACs) of one launch / its mean "
                          "duration; peak = 2500 TFLOP/s dense fp16 MFMA / 3 split passes")
@@ -651,12 +660,19 @@ def psnr(a, b):
     return 100.0 if mse < 1e-10 else 20 * math.log10(1.0 / math.sqrt(mse))
 
 
-def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
+def cpu_baseline(torch, model, vox, H, W, n_frames, timed=None, n_last=3, min_s=10.0, max_seqs=24):
     """Bounded CPU sample of the same workload: the reference's forward restated op for op on
     ATen's CPU kernels (oracle/cista_oracle_torch.py -- what the reference itself runs on a
     CPU), multi-threaded over this process's host cores, on B=1 sequences of n_frames recurrent
-    frames at full size, repeated until >= min_s seconds (at most max_seqs sequences).  Also
-    returns the GPU-vs-CPU agreement (PSNR, max relative error) on the first sequence."""
+    frames at full size, repeated until >= min_s seconds (at most max_seqs sequences).
+
+    Also returns the agreement (PSNR of utils/evaluate.py:18-28, max relative errors) of the
+    TIMED path's own frames with the CPU restatement on the same inputs: `timed` = the frames
+    the timed region produced for sequences 0 and B-1, (L, 2, 1, H, W) on the host (the
+    whole-sequence graph replay at the bench batch, with its two-region tiling and XCD item
+    order), against CPU sequence 0 over n_frames frames and CPU sequence B-1 over n_last frames.
+    Without `timed` (eager-only runs) the comparison falls back to an eager B=1 run of
+    sequence 0."""
     import numpy as np
     from oracle import fixtures as fx
     from oracle.cista_oracle_torch import CistaLSTCTorchCPU
@@ -664,11 +680,11 @@ def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
     torch.set_num_threads(cores)
     sd = {k: v.detach().cpu().numpy() for k, v in model.state_dict().items()}
     ref = CistaLSTCTorchCPU(fx.collapse_tied(sd, model.depth), model.depth)
-    L = vox.shape[0]
+    L, B = vox.shape[0], vox.shape[1]
     n_frames = min(n_frames, L)
     ref.run_sequence(vox[:1, :1].cpu().numpy())                 # warm-up (oneDNN primitives)
     frames, dt, seqs, o_recs = 0, 0.0, 0, None
-    while seqs < min(max_seqs, vox.shape[1]) and (dt < min_s or seqs == 0):
+    while seqs < min(max_seqs, B) and (dt < min_s or seqs == 0):
         v = vox[:n_frames, seqs:seqs + 1].cpu().numpy()
         t0 = time.perf_counter()
         recs, _ = ref.run_sequence(v)
@@ -677,22 +693,32 @@ def cpu_baseline(torch, model, vox, H, W, n_frames, min_s=10.0, max_seqs=24):
             o_recs = recs
         frames += n_frames
         seqs += 1
-    with torch.no_grad():
-        prev = torch.zeros(1, 1, H, W, device=vox.device)
-        states = None
-        g_recs = []
-        for f in range(n_frames):
-            prev, states = model(vox[f, :1], prev, states)
-            g_recs.append(prev.cpu().numpy())
-    g_recs = np.stack(g_recs)
-    rel = float(np.abs(g_recs - o_recs).max() / np.abs(o_recs).max())
+    pairs = []                      # (GPU frames, CPU frames), each (n, 1, 1, H, W)
+    if timed is not None:
+        pairs.append((np.asarray(timed[:n_frames, :1]), o_recs))
+        n_last = min(n_last, L)
+        last_ref, _ = ref.run_sequence(vox[:n_last, B - 1:B].cpu().numpy())
+        pairs.append((np.asarray(timed[:n_last, 1:2]), last_ref))
+        what = (f"the timed graph replay's frames of sequence 0 ({n_frames} frames) and sequence {B - 1} "
+                f"({n_last} frames) at B={B}")
+    else:
+        with torch.no_grad():
+            prev = torch.zeros(1, 1, H, W, device=vox.device)
+            states = None
+            g_recs = []
+            for f in range(n_frames):
+                prev, states = model(vox[f, :1], prev, states)
+                g_recs.append(prev.cpu().numpy())
+        pairs.append((np.stack(g_recs), o_recs))
+        what = f"an eager B=1 run of sequence 0 ({n_frames} frames)"
+    rel = max(float(np.abs(g - o).max() / np.abs(o).max()) for g, o in pairs)
     # SURVEY 7's frame metric: per pixel, each against its own magnitude
-    erel = float((np.abs(g_recs.astype(np.float64) - o_recs) / np.maximum(np.abs(o_recs), 1e-30)).max())
-    ps = float(np.mean([psnr(g_recs[f], o_recs[f]) for f in range(n_frames)]))
+    erel = max(float((np.abs(g.astype(np.float64) - o) / np.maximum(np.abs(o), 1e-30)).max()) for g, o in pairs)
+    ps = float(np.mean([psnr(g[f], o[f]) for g, o in pairs for f in range(len(o))]))
     return dict(value=frames / dt, unit="frames/s", cores=int(cores), kind="port",
                 sample=f"{seqs} sequence(s) x {n_frames} recurrent frames at {H}x{W} (B=1), "
                        f"PyTorch-CPU op-for-op restatement (oracle/cista_oracle_torch.py), "
-                       f"{core_note}, {dt:.1f} s"), ps, rel, erel
+                       f"{core_note}, {dt:.1f} s"), ps, rel, erel, what
 
 
 def frame_work(lib_mod, model, H, W):
@@ -747,14 +773,129 @@ def batch_sweep(torch, model, args, device, batches):
     return out
 
 
+def pg_info(vd):
+    """The ranks the process group actually holds and its backend (nccl = RCCL on ROCm); a
+    single process without a launcher has no group: 1 rank, None."""
+    import torch.distributed as dist
+    return {"ranks_seen": dist.get_world_size() if vd.active() else 1,
+            "process_group": dist.get_backend() if vd.active() else None}
+
+
+def _free_port():
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch_ranks(n, argv, poll_s=0.2):
+    """bench.py --gpus N (N > 1) started without a rank launcher: N fresh child interpreters
+    running this script, one rank per GPU (RANK = LOCAL_RANK = i, WORLD_SIZE = N, MASTER_* on
+    127.0.0.1, and the launcher marker v2e2v_amd.dist reads), the role torchrun plays for the
+    driver's scaling runs.  The parent never touches the GPU and never execs: it waits on its
+    children, and as soon as one fails it stops the others (their exact PIDs) so no rank is
+    left waiting in a collective.  Returns the exit code: 0 only if every rank exited 0.
+    Replaces the reference's single-GPU picker (train_e2v.py:3-14, test_e2v.py:2-13)."""
+    import subprocess
+    from v2e2v_amd.dist import LAUNCHER_ENV
+    port = str(_free_port())
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
+                   MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
+        env[LAUNCHER_ENV] = "bench.py"
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+    rc = 0
+    try:
+        while [p.poll() for p in procs].count(None):
+            bad = [p.returncode for p in procs if p.returncode not in (None, 0)]
+            if bad:
+                rc = bad[0]
+                break
+            time.sleep(poll_s)
+        else:
+            rc = next((p.returncode for p in procs if p.returncode != 0), 0)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.terminate()
+        for p in procs:
+            try:
+                p.wait(timeout=30)
+            except subprocess.TimeoutExpired:
+                p.kill()
+                p.wait()
+    if rc != 0:
+        print(f"bench.py: a rank failed (exit {rc}); {n}-rank run aborted", file=sys.stderr)
+    return 0 if rc == 0 else (rc if rc > 0 else 128 - rc)
+
+
+def rank_plan(args):
+    """How this process takes part: ("launch", N) -- start N ranks (launch_ranks); ("rank", N) --
+    one rank of an N-rank job set up by a launcher (torchrun or launch_ranks); ("single", 1).
+    A launcher's WORLD_SIZE must agree with --gpus when both are given: a mismatch raises
+    SystemExit(2), so a scaling run can never report the wrong number of GPUs."""
+    from v2e2v_amd import dist as vd
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    launched = vd.under_launcher() or world > 1
+    if launched:
+        if args.gpus is not None and args.gpus != world:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={world} "
+                             f"ranks; refusing to report a {world}-rank run as {args.gpus} GPUs")
+        args.gpus = world
+        return "rank", world
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        raise SystemExit(f"bench.py: --gpus {n}")
+    args.gpus = n
+    return ("launch", n) if n > 1 else ("single", 1)
+
+
+def dry_run_main(args, vd):
+    """--dry-run: the rank plumbing alone, on CPU over gloo (no HIP call): barrier, K timed
+    trivial steps, max over ranks, rank 0 prints the line the real bench would shape."""
+    import torch
+    import torch.distributed as dist
+    if os.environ.get("V2E2V_DRY_FAIL_RANK") == os.environ.get("RANK", "0"):
+        raise SystemExit(3)         # test hook: this rank dies before the process group forms
+    rank, world, _ = vd.init("gloo")
+    x = torch.ones(4096)
+    vd.barrier()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        x = x * 1.0001
+    vd.barrier()
+    elapsed = vd.max_over_ranks(time.perf_counter() - t0)
+    pids = [os.getpid()]
+    if vd.active():
+        pids = [None] * world
+        dist.all_gather_object(pids, os.getpid())
+    if rank == 0:
+        print(json.dumps({"metric": "launcher dry run (no GPU work)", "value": round(world * args.steps / max(elapsed, 1e-9), 2),
+                          "unit": "steps/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+                          "ranks_seen": dist.get_world_size() if vd.active() else 1,
+                          "process_group": dist.get_backend() if vd.active() else None,
+                          "rank_pids": pids}), flush=True)
+    vd.finalize()
+
+
 def main():
     args = parse()
+    role, n = rank_plan(args)
+    if role == "launch":
+        sys.exit(launch_ranks(n, sys.argv[1:]))
+    from v2e2v_amd import dist as vd
+    if args.dry_run:
+        return dry_run_main(args, vd)
     import torch
     from v2e2v_amd import CistaLSTCNet, _lib
-    from v2e2v_amd import dist as vd
     from v2e2v_amd.sequence import CistaSequence
 
     rank, world, local_rank = vd.env_rank()
+    if world > 1 and torch.cuda.device_count() < world:
+        raise SystemExit(f"bench.py: {world} ranks but {torch.cuda.device_count()} visible GPU(s)")
     device = torch.device("cuda", local_rank)
     torch.cuda.set_device(device)
     vd.init("nccl", device)
@@ -791,6 +932,9 @@ def main():
     rec = timings[path][1]
     rec = rec[0] if isinstance(rec, tuple) else rec
     finite = bool(torch.isfinite(rec).all())
+    # the timed replay's own frames of the first and last sequence (every frame of the last
+    # replay; each step replays the same inputs), kept for the parity check against the CPU path
+    timed_recs = seq.recs[:, [0, B - 1]].cpu().numpy() if path == "graph" else None
     frames = world * B * L * args.steps
     value = frames / elapsed
 
@@ -801,10 +945,10 @@ def main():
                  if rank == 0 else None)
 
     cpu = None
-    psnr_vs_ref = rel_vs_ref = erel_vs_ref = None
+    psnr_vs_ref = rel_vs_ref = erel_vs_ref = parity_sample = None
     if rank == 0 and not args.no_cpu_baseline:
-        cpu, psnr_vs_ref, rel_vs_ref, erel_vs_ref = cpu_baseline(torch, model, vox, H, W,
-                                                    min(args.cpu_frames, L))
+        cpu, psnr_vs_ref, rel_vs_ref, erel_vs_ref, parity_sample = cpu_baseline(
+            torch, model, vox, H, W, min(args.cpu_frames, L), timed=timed_recs)
 
     if rank == 0:
         frame_ms = sum(v["ms"] * v["launches_per_frame"] for v in layers.values())
@@ -819,6 +963,7 @@ def main():
             "value": round(value, 2),
             "unit": "frames/s",
             "n_gpus": world,
+            **pg_info(vd),
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(elapsed / args.steps * 1e3, 3),
@@ -849,6 +994,7 @@ def main():
             "psnr_vs_ref": None if psnr_vs_ref is None else round(psnr_vs_ref, 2),
             "max_rel_err_vs_ref": rel_vs_ref,
             "max_elementwise_rel_err_vs_ref": erel_vs_ref,
+            "parity_sample": parity_sample,
             "outputs_finite": finite,
             "roofline": roofline,
             "cpu_baseline": cpu,

@@ -54,7 +54,8 @@ def test_gloo_sharding_and_reductions(world):
 def _single_worker(port, q):
     # torchrun --nproc-per-node 1 sets the rank environment at world size 1: the process group
     # must still come up (the N=1 scaling point runs the same DDP all-reduce as N=8)
-    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    os.environ.update(RANK="0", WORLD_SIZE="1", LOCAL_RANK="0", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                      TORCHELASTIC_RUN_ID="test")
     r, w, _ = vd.init("gloo")
     up = vd.active()
     m = torch.nn.Linear(3, 2)
@@ -79,11 +80,26 @@ def test_world_size_one_under_launcher_initialises_process_group():
 
 
 def test_no_process_group_without_launcher(monkeypatch):
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT"):
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_PORT", "TORCHELASTIC_RUN_ID", vd.LAUNCHER_ENV):
         monkeypatch.delenv(k, raising=False)
     assert not vd.under_launcher()
     assert vd.init("gloo") == (0, 1, 0)
     assert not vd.active()
+
+
+def test_scheduler_rank_env_at_world_one_is_not_a_launcher(monkeypatch):
+    """A scheduler / MPI wrapper that exports WORLD_SIZE=1 and MASTER_PORT is not torchrun:
+    the process stays single-process (no TCPStore, no DDP wrap)."""
+    for k in ("TORCHELASTIC_RUN_ID", vd.LAUNCHER_ENV):
+        monkeypatch.delenv(k, raising=False)
+    monkeypatch.setenv("WORLD_SIZE", "1")
+    monkeypatch.setenv("RANK", "0")
+    monkeypatch.setenv("MASTER_PORT", "29999")
+    assert not vd.under_launcher()
+    assert vd.init("gloo") == (0, 1, 0)
+    assert not vd.active()
+    monkeypatch.setenv("TORCHELASTIC_RUN_ID", "x")
+    assert vd.under_launcher()
 
 
 def test_shard_partition_properties():

@@ -218,7 +218,8 @@ def _worker_nccl1(_idx, port, out_dir):
     """One RCCL ("nccl") rank at world size 1, as torchrun --nproc-per-node 1 runs bench.py
     --mode train: the DDP-wrapped 3-frame BPTT step must give the unwrapped model's gradients
     bit for bit (the all-reduce over one rank divides by 1)."""
-    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0",
+                      TORCHELASTIC_RUN_ID="test")
     sys.path.insert(0, ROOT)
     import torch
 

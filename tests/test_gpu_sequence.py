@@ -55,3 +55,29 @@ def test_graph_replay_bit_identical_to_eager(B, H, W, L):
     r3, _ = seq2.run()
     ref3, _ = eager(m, vox, prev, states)
     assert torch.equal(r3, ref3) and not torch.equal(r3, r2)
+
+
+def test_graph_replay_two_region_batch_bit_identical():
+    """The bench's timed configuration in small: a whole-sequence graph replay at a batch where
+    the forward convs tile in two regions (B=20 at 180x240: 20 x 57 items >= 1024, checked
+    through cista_tile_plan) gives the eager B=20 loop's frames and states bit for bit, and
+    each of its sequences equals that sequence run alone at B=1 (one region, small-batch tiles)."""
+    import ctypes
+    from v2e2v_amd import _lib
+    B, H, W, L = 20, 180, 240, 3
+    out = (ctypes.c_int * 14)()
+    assert _lib.lib().cista_tile_plan(B, H // 2, W // 2, 192, out) == 0 and out[8] > 0      # region b present
+    assert _lib.lib().cista_tile_plan(1, H // 2, W // 2, 192, out) == 0 and out[8] == 0     # B=1: one region
+    m = model(H, W)
+    vox = torch.from_numpy(fx.synthetic_voxels(L, B, 5, H, W, n_events=15000, seed=11)).to(DEV)
+    seq = CistaSequence(m, vox)
+    recs, st = seq.run()
+    torch.cuda.synchronize()
+    ref, rst = eager(m, vox, torch.zeros(B, 1, H, W, device=DEV), None)
+    assert torch.equal(recs, ref)
+    for a, b in zip([st[0], st[1], st[2][0], st[2][1]], [rst[0], rst[1], rst[2][0], rst[2][1]]):
+        assert torch.equal(a, b)
+    for s in (0, B - 1):
+        one, ost = eager(m, vox[:, s:s + 1].contiguous(), torch.zeros(1, 1, H, W, device=DEV), None)
+        assert torch.equal(recs[:, s:s + 1], one)
+        assert torch.equal(st[1][s:s + 1], ost[1]) and torch.equal(st[2][1][s:s + 1], ost[2][1])

@@ -45,7 +45,7 @@ ConvShape conv_shape(int id, int C) {
 struct Layout {
     size_t wp[CV_COUNT], bp[CV_COUNT], sc[CV_COUNT];
     size_t dwp[CV_COUNT], dbp[CV_COUNT];   // dgrad B fragments (flipped, transposed) + zero bias
-    size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS, wU4, bU4, wUT, bU;
+    size_t wE, wI, bIn, wF, bF, lambda, wC, bC, wS, bS, wU4, bU4;
     size_t w4p, b4p;                       // W0 dgrad as a four-phase conv (pack_w0phase_kernel)
     size_t wsp;                            // weight |max| partials of the pack (weight_absmax_kernel)
     size_t total;
@@ -83,8 +83,6 @@ Layout make_layout(const cista_config &cfg) {
     L.bS = off; off = align_up(off + (size_t)C * 4);
     L.wU4 = off; off = align_up(off + (size_t)4 * C * C * 9 * 4);        // CV_UP4, reference layout
     L.bU4 = off; off = align_up(off + (size_t)4 * C * 4);
-    L.wUT = off; off = align_up(off + (size_t)C * C * 9 * 4);            // upsample W as [ci*9+t][co]
-    L.bU = off; off = align_up(off + (size_t)C * 4);
     L.w4p = off; off = align_up(off + (size_t)(C / 32) * 9 * (4 * C / 16) * 2 * 64 * 16);
     L.b4p = off; off = align_up(off + (size_t)4 * C * 4);
     L.wsp = off; off = align_up(off + (size_t)CV_COUNT * WS_PARTS * 4);
@@ -144,10 +142,6 @@ size_t lds_bytes(int TH, int TW, int S) {
     return (size_t)((HP + 15) & ~15) * 8 * 16;
 }
 
-#ifndef CISTA_MSEG
-#define CISTA_MSEG 1      // row-aligned m-tiles for stride-1 convs (0: row-major only, A/B builds)
-#endif
-
 // One tile candidate: TW columns, row-major m-tiles (mode 0) or row-aligned m-tile segments
 // (mode 1), as many rows as the workgroup's pixels, the staging registers (max_items: halo
 // items, HP rounded to 8, x4 k-groups, one workgroup may hold; 0 = unlimited) and the LDS
@@ -162,6 +156,11 @@ bool tile_candidate(int Hout, int Wout, int block_px, int S, int max_items, int 
     auto items = [&](int th) { return ((((th - 1) * S + 3) * ((TW - 1) * S + 3) + 7) & ~7) * 4; };
     while (max_items && TH > 1 && items(TH) > max_items) --TH;
     if (max_items && items(TH) > max_items) return false;
+    // the kernel's small_div range (ConvArgs.rcp_pitch, the halo coordinates): halo < 2048
+    // pixels, pitch and halo width <= 512 -- a tile outside it is never ranked (launch_conv_cfg
+    // would refuse it)
+    if (((TH - 1) * S + 3) * ((TW - 1) * S + 3) >= 2048 || (mode ? 16 * mseg : TW) > 512 || (TW - 1) * S + 3 > 512)
+        return false;
     const size_t lds = lds_bytes(TH, TW, S) * nbuf;
     if (lds > 160 * 1024 / (size_t)occ) return false;
     t = Tile{TH, TW, (Hout + TH - 1) / TH, (Wout + TW - 1) / TW, lds, mseg};
@@ -184,12 +183,8 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
     double best_eff = -1.0, best_cost = 1e300;
     int best_conf = 1;
     size_t best_lds = ~(size_t)0;
-    for (int mode = 0; mode < ((seg && CISTA_MSEG) ? 2 : 1); ++mode)
+    for (int mode = 0; mode < (seg ? 2 : 1); ++mode)
     for (int TW = 1; TW <= block_px && TW <= Wout; ++TW) {
-#if CISTA_TW16
-        // 16-pixel m-tiles that never wrap a tile row read LDS without bank conflicts
-        if (Wout >= 16 && (TW % 16) != 0) continue;
-#endif
         Tile t;
         int conf;
         if (!tile_candidate(Hout, Wout, block_px, S, max_items, nbuf, occ, TW, mode, t, conf)) continue;
@@ -222,23 +217,24 @@ Tile choose_tile(int Hout, int Wout, int block_px, int S, int max_items, int nbu
 // region b's items after region a's: 54 + 3 = 57 tiles per 90 x 120 image instead of 60 (0.987),
 // the 96-pixel convs 105 + 8 = 113 instead of 115.  Only where the launch is at least two
 // dispatch rounds (B x tiles >= 1024 items on 512 workgroup slots): a one-round launch takes one
-// workgroup lifetime whatever its item count.  Memoised per shape.
-#ifndef CISTA_SPLIT
-#define CISTA_SPLIT 1
-#endif
+// workgroup lifetime whatever its item count.  Memoised per shape in a 64-entry table with
+// round-robin replacement (a process serving many resolutions re-plans a shape it evicted,
+// ~0.1 ms of host time, instead of re-planning every unseen shape forever); use_cache = false
+// (cista_tile_plan introspection) neither reads nor fills it.
 struct TilePlan { Tile a, b; int wa; };   // b.tx == 0: one region (a covers every column)
 
 TilePlan plan_tiles(int B, int Hout, int Wout, int block_px, int S, int max_items, int nbuf, int occ, bool seg,
-                    double halo_w) {
+                    double halo_w, bool use_cache = true) {
     TilePlan best{choose_tile(Hout, Wout, block_px, S, max_items, nbuf, occ, seg, halo_w), Tile{}, Wout};
-    if (!CISTA_SPLIT || halo_w > 0.0 || (long)B * best.a.ty * best.a.tx < 1024) return best;
+    if (halo_w > 0.0 || (long)B * best.a.ty * best.a.tx < 1024) return best;
     struct Key { int Hout, Wout, block_px, S, max_items, nbuf, occ, seg; };
     struct Ent { Key k; TilePlan p; };
     static std::mutex mu;
-    static Ent cache[64];
-    static int ncache = 0;
+    constexpr int NCACHE = 64;
+    static Ent cache[NCACHE];
+    static int ncache = 0, next = 0;
     const Key key{Hout, Wout, block_px, S, max_items, nbuf, occ, seg ? 1 : 0};
-    {
+    if (use_cache) {
         std::lock_guard<std::mutex> lock(mu);
         for (int i = 0; i < ncache; ++i)
             if (!memcmp(&cache[i].k, &key, sizeof(Key))) return cache[i].p;
@@ -253,7 +249,7 @@ TilePlan plan_tiles(int B, int Hout, int Wout, int block_px, int S, int max_item
         if (tile_candidate(Hout, Wout, block_px, S, max_items, nbuf, occ, best.a.TW, best.a.mseg ? 1 : 0, t, conf))
             best_conf = conf ? best_tiles : 0;
     }
-    for (int mode = 0; mode < ((seg && CISTA_MSEG) ? 2 : 1); ++mode)
+    for (int mode = 0; mode < (seg ? 2 : 1); ++mode)
         for (int TW = 1; TW <= block_px && TW < Wout; ++TW) {
             const int wa = (Wout / TW) * TW;
             if (wa == Wout) continue;
@@ -271,8 +267,13 @@ TilePlan plan_tiles(int B, int Hout, int Wout, int block_px, int S, int max_item
                 best = TilePlan{ta, tb, wa};
             }
         }
+    if (!use_cache) return best;
     std::lock_guard<std::mutex> lock(mu);
-    if (ncache < 64) cache[ncache++] = Ent{key, best};
+    for (int i = 0; i < ncache; ++i)                 // another thread planned it meanwhile
+        if (!memcmp(&cache[i].k, &key, sizeof(Key))) return cache[i].p;
+    cache[next] = Ent{key, best};
+    next = (next + 1) % NCACHE;
+    if (ncache < NCACHE) ++ncache;
     return best;
 }
 
@@ -379,31 +380,14 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     return CISTA_OK;
 }
 
-// pick the wave tiling from the number of packed output columns.
-// CISTA_VARIANT selects the tiling family (A/B builds for scripts/layer_bench.py):
-//   0: MT_W=8 x NW=4 waves, no B prefetch
-//   1: MT_W=16 x NW=2 waves with B-fragment prefetch where the epilogue allows NW=2
-//   2: double-buffered K loop (next halo chunk prefetched into registers), B prefetch
-#ifndef CISTA_VARIANT
-#define CISTA_VARIANT 2
-#endif
-#ifndef CISTA_TW16
-#define CISTA_TW16 0
-#endif
-#ifndef CISTA_PF_MT
-#define CISTA_PF_MT 12
-#endif
+// pick the wave tiling from the number of packed output columns: the direct stagings (reflect /
+// zero / space-to-depth) run the double-buffered K loop (the next halo chunk prefetched into
+// registers, B-fragment prefetch); the bilinear staging of C not in {32, 64} a single-buffered one
 #ifndef CISTA_SMALL_GRID
 #define CISTA_SMALL_GRID 1   // latency tiles for grids that would not fill the chip (small B)
 #endif
 #ifndef CISTA_W0_PHASE
 #define CISTA_W0_PHASE 1         // W0's dgrad as a four-phase MFMA conv (0: the VALU dgrad_s2_kernel)
-#endif
-#ifndef CISTA_DGRAD_SMALL
-#define CISTA_DGRAD_SMALL 0      // > 0: dgrad launches below this many throughput workgroups use 64 x 64 tiles (1024 measured slower at B = 8)
-#endif
-#ifndef CISTA_WIDE
-#define CISTA_WIDE 1      // forward N % 256 convs (gates, ConvLSTM) on <6,4,1,4>; 0: A/B builds
 #endif
 // fewer than ~1.5 workgroups per CU with the throughput configuration (px x cols per WG)
 inline bool small_grid(const ConvArgs &a, int wg_px, int wg_cols, int limit = 384) {
@@ -430,15 +414,9 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
         if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
         if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (CISTA_VARIANT == 2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_S2D)) {
+    } else if constexpr (STAGE == STAGE_S1 || STAGE == STAGE_ZP2 || STAGE == STAGE_S2D) {
         // double-buffered K loop, 192-pixel workgroups, halo items in 4 x 8 VGPRs per thread
         constexpr bool FWD = STAGE == STAGE_S1 || STAGE == STAGE_S2D;
-        if constexpr (STAGE == STAGE_ZP2 && G == 1) {
-            // training dgrads at small batches (B = 8): below ~4 throughput workgroups per CU
-            // the launch is one workgroup lifetime long; 64 x 64 workgroups give 4x as many
-            if (a.N % 64 == 0 && small_grid(a, 192, a.N % 128 == 0 ? 128 : 64, CISTA_DGRAD_SMALL))
-                return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
-        }
         if constexpr (FWD) {
             // small batches (B = 1 is the reference harness's case): the throughput tiles below
             // leave most CUs idle, so 64-pixel x 64-column workgroups trade MFMA efficiency
@@ -449,7 +427,7 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
                 else return launch_conv_cfg<2, 2, 2, 2, STAGE, EPI, G, true, 2>(a, st);
             }
         }
-        if constexpr (FWD && CISTA_WIDE)      // one workgroup holds all 256 columns, 96 pixels
+        if constexpr (FWD)      // one workgroup holds all 256 columns, 96 pixels
             if (a.N % 256 == 0) return launch_conv_cfg<6, 4, 1, 4, STAGE, EPI, G, true, 4>(a, st);
         if constexpr (G == 4) {
             if (a.N % 128 == 0) return launch_conv_cfg<6, 4, 2, 2, STAGE, EPI, G, true, 4>(a, st);
@@ -459,19 +437,12 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
             if (a.N % 32 == 0) return launch_conv_cfg<3, 2, 4, 1, STAGE, EPI, G, true, 4>(a, st);   // N = 32, 96, 160 ...
         }
         return CISTA_ERR_UNSUPPORTED;
-    } else if constexpr (CISTA_VARIANT >= 1 && G <= 2) {
-        constexpr int MT = CISTA_PF_MT;
-        if (a.N % 128 == 0) return launch_conv_cfg<MT, 2, 1, 4, STAGE, EPI, G, true>(a, st);
-        if (a.N % 64 == 0) return launch_conv_cfg<MT, 2, 2, 2, STAGE, EPI, G, true>(a, st);
-        if (a.N % 32 == 0) return launch_conv_cfg<MT, 2, 4, 1, STAGE, EPI, G, true>(a, st);
+    } else if constexpr (G <= 2) {      // STAGE_UP + EPI_RELU (upsample conv of C not in {32, 64})
+        if (a.N % 128 == 0) return launch_conv_cfg<12, 2, 1, 4, STAGE, EPI, G, true>(a, st);
+        if (a.N % 64 == 0) return launch_conv_cfg<12, 2, 2, 2, STAGE, EPI, G, true>(a, st);
+        if (a.N % 32 == 0) return launch_conv_cfg<12, 2, 4, 1, STAGE, EPI, G, true>(a, st);
         return CISTA_ERR_UNSUPPORTED;
     } else {
-        if (a.N >= 256 && a.N % 256 == 0) return launch_conv_cfg<8, 4, 1, 4, STAGE, EPI, G>(a, st);
-        if (a.N >= 128 && a.N % 128 == 0) return launch_conv_cfg<8, 4, 2, 2, STAGE, EPI, G>(a, st);
-        if constexpr (G <= 2) {
-            if (a.N == 64) return launch_conv_cfg<8, 4, 4, 1, STAGE, EPI, G>(a, st);
-            if (a.N == 32) return launch_conv_cfg<8, 2, 4, 1, STAGE, EPI, G>(a, st);
-        }
         return CISTA_ERR_UNSUPPORTED;
     }
 }
@@ -567,9 +538,6 @@ inline bool up_q_path(int C) { return C == 64 || C == 32; }
 #define CISTA_UP4 1
 #endif
 inline bool up4_path(int C) { return CISTA_UP4 && C == 64; }
-#ifndef CISTA_UP4_BORDER_VALU
-#define CISTA_UP4_BORDER_VALU 0   // 1: the border pixels by up_border_kernel (VALU) instead
-#endif
 
 ConvArgs conv_args_f(const Frame &f, int id, int C, int B, int Hin, int Win, int Hout, int Wout,
                      const float *in0, int c0, const float *in1, int c1) {
@@ -744,15 +712,6 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 const int sc = f.u ? launch_conv<STAGE_CLAMP, EPI_UP4_Q_SAVE, 1>(a, f.st)
                                    : launch_conv<STAGE_CLAMP, EPI_UP4_Q, 1>(a, f.st);
                 if (sc) return sc;
-#if CISTA_UP4_BORDER_VALU
-                UpBorderArgs ub;
-                ub.h = f.hs; ub.wt = blob<float>(f.packed, f.L.wUT); ub.bias = blob<float>(f.packed, f.L.bU);
-                ub.wf = blob<float>(f.packed, f.L.wF);
-                ub.q = f.full; ub.u = f.u; ub.B = B; ub.H = f.H; ub.W = f.W; ub.C = C;
-                const long nbp = (long)B * (2 * f.W + 2 * (f.H - 2));
-                hipLaunchKernelGGL(up_border_kernel, dim3((unsigned)nbp), dim3(64), (size_t)9 * C * 4, f.st, ub);
-                return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
-#else
                 // border strips: the bilinear-staging upsample conv (exact reference arithmetic)
                 // on 1-row / 1-column tiles, one fixed configuration for every batch size
                 for (int mode = 1; mode <= 2; ++mode) {
@@ -767,7 +726,6 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                     if (sb) return sb;
                 }
                 return CISTA_OK;
-#endif
             }
             a = conv_args_f(f, CV_UP, C, B, h, w, f.H, f.W, f.hs, C, nullptr, 0);
             a.out0 = f.full;
@@ -1260,6 +1218,7 @@ int dgrad_conv(Bwd &k, int id, const float *G, float *dxp, const float *sc = nul
 #ifndef CISTA_FOLD_EPI
 #define CISTA_FOLD_EPI 1   // dgrads fold the reflect padding in their epilogue (0: fold_reflect_kernel pass)
 #endif
+constexpr int FOLD_COL_ALIGN = 32;      // NW * 16 of the STAGE_ZP2 wave tilings
 
 FoldSeg fseg(float *dst, int Cd, int dc0, float scale = 1.0f, int mode = FOLD_SET, float *aux = nullptr,
              unsigned *amax = nullptr) {
@@ -1274,7 +1233,9 @@ FoldSeg fseg(float *dst, int Cd, int dc0, float scale = 1.0f, int mode = FOLD_SE
 int dgrad_fold(Bwd &k, int id, const float *G, const float *sc, const FoldSeg &s0, const FoldSeg &s1, int split) {
     const ConvShape s = conv_shape(id, k.C);
     const int Hin = id == CV_UP ? k.H : k.h, Win = id == CV_UP ? k.W : k.w;
-    if (Hin < 4 || Win < 4 || split % 16) return CISTA_ERR_UNSUPPORTED;
+    // a wave's NW x 16 columns must lie in one FoldSeg: every STAGE_ZP2 configuration of
+    // launch_conv has NW = 2 (checked again by launch_conv_cfg)
+    if (Hin < 4 || Win < 4 || split % FOLD_COL_ALIGN) return CISTA_ERR_UNSUPPORTED;
     ConvArgs a;
     memset(&a, 0, sizeof(a));
     a.in0 = G; a.c0 = s.cout; a.in1 = nullptr; a.c1 = 0;
@@ -1321,7 +1282,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     hipStream_t st = k.st;
     // the reflect fold in the dgrad epilogue (dgrad_fold) needs input rows 1 and n-2 distinct
     // (n, m >= 4); smaller images take the padded-domain dgrad + fold_reflect_kernel pass
-    const bool fold_half = CISTA_FOLD_EPI && h >= 4 && w >= 4, fold_full = CISTA_FOLD_EPI && H >= 4 && W >= 4;
+    // (and FoldSeg splits at multiples of a wave's columns: C, 2C with C % 32 == 0 -- cfg_supported)
+    const bool fold_ok = CISTA_FOLD_EPI && C % FOLD_COL_ALIGN == 0;
+    const bool fold_half = fold_ok && h >= 4 && w >= 4, fold_full = fold_ok && H >= 4 && W >= 4;
     // ---- 1-2. output stage: rec = sigmoid(final_conv(u)), u = relu(upsamp_conv(up(h))) --------
     CHECK(copy_or_zero(ws.ghb, g.g_h, (size_t)hw * C, st));
     if (g.g_rec) {
@@ -1685,14 +1648,11 @@ int cista_pack_params(const cista_config *cfg, const cista_params *p, void *pack
                        p->Wi_w, blobw<float>(packed, L.wI), half, 1);
     hipLaunchKernelGGL(final_weight_kernel, dim3((C * 9 + 255) / 256), dim3(256), 0, st,
                        p->final_w, blobw<float>(packed, L.wF), C);
-    hipLaunchKernelGGL(transpose_small_kernel, dim3((C * C * 9 + 255) / 256), dim3(256), 0, st,
-                       p->up_w, blobw<float>(packed, L.wUT), C, C);
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     char *pb = static_cast<char *>(packed);
     if (hipMemcpyAsync(pb + L.bIn, p->We_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.bIn + half * 4, p->Wi_b, half * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.bF, p->final_b, 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
-        hipMemcpyAsync(pb + L.bU, p->up_b, (size_t)C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess ||
         hipMemcpyAsync(pb + L.lambda, p->lambda, 2 * C * 4, hipMemcpyDeviceToDevice, st) != hipSuccess)
         return CISTA_ERR_HIP;
     return CISTA_OK;
@@ -1864,7 +1824,7 @@ int cista_tile_plan(int B, int Hout, int Wout, int block_px, int *out) {
     if (!out || B < 1 || Hout < 1 || Wout < 1 || (block_px != 192 && block_px != 96)) return CISTA_ERR_INVALID;
     // the forward double-buffered configurations: NI = 4 halo items per thread x 256 threads,
     // two LDS images, two workgroups per CU, row-aligned m-tiles allowed (launch_conv_cfg)
-    const TilePlan p = plan_tiles(B, Hout, Wout, block_px, 1, 4 * 256, 2, 2, true, 0.0);
+    const TilePlan p = plan_tiles(B, Hout, Wout, block_px, 1, 4 * 256, 2, 2, true, 0.0, false);
     const Tile *t[2] = {&p.a, &p.b};
     for (int r = 0; r < 2; ++r) {
         out[5 * r + 0] = t[r]->TH; out[5 * r + 1] = t[r]->TW; out[5 * r + 2] = t[r]->ty;

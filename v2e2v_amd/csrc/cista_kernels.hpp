@@ -2076,7 +2076,7 @@ __global__ __launch_bounds__(256) void final_stage_kernel(const FinalArgs a) {
 // N = 4C columns of one implicit GEMM, with NO per-pixel interpolation.  Bilinear's index clamp
 // is edge replication of h (STAGE_CLAMP).  ReflectionPad2d(1) of the full-res image is not
 // expressible that way: the output rows 0, H-1 and columns 0, W-1 are recomputed exactly by
-// up_border_kernel after the conv.
+// the bilinear-staging conv (STAGE_UP, EPI_UP_Q) on 1-row / 1-column border tiles after it.
 // ------------------------------------------------------------------------------------------
 __device__ __forceinline__ double up_phase_w(int a, int d, int r) {
     // A[a][d][r]: weight of half-res row i + r - 1 in upsampled row 2i + a + d - 1
@@ -2101,65 +2101,6 @@ __global__ void compose_up4_kernel(const float *W, const float *b, float *W4, fl
         for (int dx = 0; dx < 3; ++dx)
             acc += (double)W[((size_t)co * C + ci) * 9 + dy * 3 + dx] * up_phase_w(pa, dy, r) * up_phase_w(pb, dx, sx);
     W4[idx] = (float)acc;
-}
-
-// Border pixels of the upsample conv (full-res rows 0, H-1 and columns 0, W-1), the reference
-// arithmetic exactly: bilinear x2 of h at the ReflectionPad2d(1)-mapped positions, the 3x3 conv
-// in fp32, ReLU, then final_conv's 9 per-tap channel contractions (q planes, EPI_UP_Q layout).
-// One 64-thread workgroup per border pixel; thread = output channel(s).
-struct UpBorderArgs {
-    const float *h;      // (B, h, w, C) NHWC
-    const float *wt;     // [C_in * 9 + tap][C_out] (transpose_small_kernel layout: coalesced over co)
-    const float *bias;   // [C]
-    const float *wf;     // [9][C] final_conv weights
-    float *q;            // (B, 9, H, W)
-    float *u;            // optional (B, H, W, C): u for the training backward
-    int B, H, W, C;
-};
-
-__global__ __launch_bounds__(64) void up_border_kernel(const UpBorderArgs a) {
-    extern __shared__ float U[];                    // [9][C] upsampled + reflect-padded window
-    const int nb = 2 * a.W + 2 * (a.H - 2);
-    const int b = blockIdx.x / nb, k = blockIdx.x - (blockIdx.x / nb) * nb;
-    int Y, X;
-    if (k < a.W) { Y = 0; X = k; }
-    else if (k < 2 * a.W) { Y = a.H - 1; X = k - a.W; }
-    else if (k < 2 * a.W + a.H - 2) { Y = 1 + (k - 2 * a.W); X = 0; }
-    else { Y = 1 + (k - 2 * a.W - (a.H - 2)); X = a.W - 1; }
-    const int hh = a.H / 2, ww = a.W / 2, C = a.C;
-    for (int i = threadIdx.x; i < 9 * C; i += 64) {
-        const int t = i / C, c = i - t * C;
-        int Yr = Y + t / 3 - 1, Xr = X + t % 3 - 1;                       // ReflectionPad2d(1)
-        Yr = Yr < 0 ? -Yr : (Yr >= a.H ? 2 * a.H - 2 - Yr : Yr);
-        Xr = Xr < 0 ? -Xr : (Xr >= a.W ? 2 * a.W - 2 - Xr : Xr);
-        const float sy = fmaxf(((float)Yr + 0.5f) * 0.5f - 0.5f, 0.0f);
-        const float sx = fmaxf(((float)Xr + 0.5f) * 0.5f - 0.5f, 0.0f);
-        const int y0 = (int)sy, x0 = (int)sx;
-        const int y1 = y0 + (y0 < hh - 1 ? 1 : 0), x1 = x0 + (x0 < ww - 1 ? 1 : 0);
-        const float ly1 = sy - (float)y0, ly0 = 1.0f - ly1, lx1 = sx - (float)x0, lx0 = 1.0f - lx1;
-        const float *hb = a.h + (size_t)b * hh * ww * C + c;
-        U[i] = bilerp(ly0, ly1, lx0, lx1, hb[((size_t)y0 * ww + x0) * C], hb[((size_t)y0 * ww + x1) * C],
-                      hb[((size_t)y1 * ww + x0) * C], hb[((size_t)y1 * ww + x1) * C]);
-    }
-    __syncthreads();
-    float qv[9] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-    for (int co = threadIdx.x; co < C; co += 64) {
-        float s = 0.0f;
-        for (int ci = 0; ci < C; ++ci)
-#pragma unroll
-            for (int t = 0; t < 9; ++t) s = fmaf(U[t * C + ci], a.wt[(size_t)(ci * 9 + t) * C + co], s);
-        const float u = relu_(s + a.bias[co]);
-        if (a.u) a.u[(((size_t)b * a.H + Y) * a.W + X) * C + co] = u;
-#pragma unroll
-        for (int t = 0; t < 9; ++t) qv[t] = fmaf(u, a.wf[t * C + co], qv[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < 9; ++t) {
-        float v = qv[t];
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o);
-        if (threadIdx.x == 0) a.q[(((size_t)b * 9 + t) * a.H + Y) * a.W + X] = v;
-    }
 }
 
 // ------------------------------------------------------------------------------------------

@@ -89,14 +89,7 @@ struct Scratch {
     unsigned long long *nev;   // [MAXSLOTS][SLOTW / 2] partial event totals (workgroup mod MAXSLOTS)
 };
 
-#ifndef CISTA_V2E_EXP
-#define CISTA_V2E_EXP 0   // timing-only switch (results WRONG when set): 1 float log, 2 no leak draw
-#endif
-
 __device__ __forceinline__ float lin_log(float v, double f) {
-#if CISTA_V2E_EXP == 1
-    return v <= 20.0f ? v * (float)f : logf(v);
-#endif
     // emulator_utils.py:13-38 (float64, rounded to 8 decimals, half to even like torch.round)
     const double x = (double)v;
     double y = x <= 20.0 ? x * f : log(x);
@@ -171,11 +164,7 @@ __global__ __launch_bounds__(256) void v2e_diff_kernel(Call c, State s, Scratch 
             nw = (1.0f - eps) * lp_old + eps * nw;
         }
         if (leak) {                                            // subtract_leak_current (:104-124)
-#if CISTA_V2E_EXP == 2
-            const float r = 0.0f;
-#else
             const float r = randn(c.seed, c.draw0 + 8 + 2 * (unsigned long long)n, i);
-#endif
             const float rate = g.leak_rate_hz * nrate * (1.0f - g.leak_jitter_fraction * r);
             base = base - dt_frame * rate * pos;
         }

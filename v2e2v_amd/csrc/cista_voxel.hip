@@ -26,15 +26,6 @@
 
 namespace cista_vox {
 
-// timing-only switch (results WRONG when set): 1 skip the group walk, 2 skip the block sort,
-// 3 skip the grid zeroing
-#ifndef CISTA_VOX_EXP
-#define CISTA_VOX_EXP 0
-#endif
-#ifndef CISTA_VOX_FUSED
-#define CISTA_VOX_FUSED 1   // 0: keys + global radix sort + accum for every grid size (A/B builds)
-#endif
-
 constexpr int CHUNK = 8192;    // numpy ufunc buffer size: the float32 reduction runs per chunk
 constexpr int LEAF = 128;      // numpy pairwise-sum block (PW_BLOCKSIZE)
 constexpr int MAX_LEAVES = 128;
@@ -319,7 +310,7 @@ __global__ __launch_bounds__(WT) void vox_sort_kernel(const double *ev, const lo
         __syncthreads();                                                // LDS union reuse
         WinExch(L.u.exch).StripedToBlocked(key, key);
         __syncthreads();
-        if (CISTA_VOX_EXP != 2) WinSort(L.u.sort).SortBlockedToStriped(key, 0, end_bit);
+        WinSort(L.u.sort).SortBlockedToStriped(key, 0, end_bit);
         __syncthreads();
         // (t, polarity) of every event in sorted order, for the tile kernel to stream: the rows
         // are re-read in event order (coalesced, L2 / Infinity-Cache hot) in rounds of WPR
@@ -419,10 +410,7 @@ __device__ void walk_groups(const unsigned *k, int s, int e, const double2 *tps,
 // thread touches them, so they are accumulated in registers -- the same adds in the same order
 // -- and only the touched cells are stored; a lone event (most pixels) is evaluated once.  The
 // thread's positions are taken WB at a time and their event rows gathered up front.
-#ifndef CISTA_VOX_WB
-#define CISTA_VOX_WB 4
-#endif
-constexpr int WB = CISTA_VOX_WB;
+constexpr int WB = 4;
 template <bool TORCH>
 __device__ void walk_fast(const unsigned *k, int e, const double2 *tps, double first, double dT, int nb,
                           float *tile, int TP, unsigned pa) {
@@ -523,8 +511,7 @@ __global__ __launch_bounds__(TT) void vox_tile_kernel(const double *ev, const lo
     }
     for (int i = tid; i < nb * TP; i += TT) tile[i] = 0.0f;
     __syncthreads();
-    if (CISTA_VOX_EXP == 1) {
-    } else if (nseg == 1) {
+    if (nseg == 1) {
         const int *tbw = tb + (size_t)b * (TBMAX + 1);
         const int s = tbw[t], e = tbw[t + 1];
         if (spw[b]) {                      // rare: events spilled into this window's grid
@@ -1081,7 +1068,7 @@ int cista_voxelize_checked(const double *events, const long long *offsets, int B
     const long long n = (long long)num_bins * height * width;
     const unsigned long long HW = (unsigned long long)height * width;
     const long long tp = num_bins * 4 <= WTILE ? tile_pixels(num_bins) : 0;
-    if (CISTA_VOX_FUSED && HW < (1ull << 18) - 1 && tp > 0 && ((long long)HW + tp - 1) / tp <= TBMAX) {
+    if (HW < (1ull << 18) - 1 && tp > 0 && ((long long)HW + tp - 1) / tp <= TBMAX) {
         // per-window sort + tiled accumulation (no memset, no global sort)
         if (!big_lds(reinterpret_cast<const void *>(vox_sort_kernel))) return CISTA_ERR_HIP;
         const int ntiles = (int)(((long long)HW + tp - 1) / tp);

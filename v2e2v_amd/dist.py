@@ -20,10 +20,16 @@ def env_rank():
             int(os.environ.get("LOCAL_RANK", 0)))
 
 
+LAUNCHER_ENV = "V2E2V_RANK_LAUNCHER"      # set by bench.py's own rank launcher (bench.py --gpus N)
+
+
 def under_launcher() -> bool:
-    """True when a launcher (torchrun / torch.distributed.run) set up the rank environment --
-    also at --nproc-per-node 1, where the process group still runs (one RCCL rank)."""
-    return "WORLD_SIZE" in os.environ and "MASTER_PORT" in os.environ
+    """True when a rank launcher started this process -- torchrun / torch.distributed.run (its
+    elastic agent exports TORCHELASTIC_RUN_ID to every worker) or bench.py's own --gpus N
+    launcher (LAUNCHER_ENV) -- also at world size 1, where the process group still runs (one
+    RCCL rank).  WORLD_SIZE / MASTER_PORT alone do not count: scheduler and MPI wrappers export
+    those too, and a world-size-1 job under one of them stays single-process."""
+    return "WORLD_SIZE" in os.environ and ("TORCHELASTIC_RUN_ID" in os.environ or LAUNCHER_ENV in os.environ)
 
 
 def init(backend: str | None = None, device: torch.device | None = None):
