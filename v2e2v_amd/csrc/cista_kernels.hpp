@@ -52,6 +52,12 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_XCD
 #define CISTA_XCD 1
 #endif
+// the double-buffered K loop of the stride-1 forward waves with <= 48 accumulator VGPRs (ISTA D,
+// Dg) reads the A fragments two (tap, m-tile) steps ahead instead of one m-tile ahead (DESIGN.md
+// 4.9; 1 = on, the default; 0 = mfma_tap everywhere, for A/B builds)
+#ifndef CISTA_KPIPE
+#define CISTA_KPIPE 1
+#endif
 // Diagnostic build only (CISTA_STAMPS=1, scripts/stamps.py): lane 0 of every conv wave records
 // shader-clock timestamps of its phases into g_cista_stamps[(block * 4 + wave) * 24 + slot]:
 // 0 hw id | xcc << 32, 1 start, 2 prologue staged, 3 + k end of K-chunk k (k < 8), 11 MFMA loop
@@ -1017,6 +1023,52 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                     bl[t][n] = wp[(size_t)t * tapstride + n * 128 + 64];
                 }
             float4 sv0[NI], sv1[NI];
+#if CISTA_KPIPE
+            if constexpr (STAGE == STAGE_S1 && EPI != EPI_PH4 && (MT_W * NW * 4 <= 48 || CISTA_KPIPE >= 2)) {
+                // A (pixel) fragments AH = 2 (tap, m-tile) steps ahead across tap boundaries
+                // (mfma_tap reads one m-tile ahead, ~2 MFMAs before use); same products, same order.
+                // AL: the lo fragment's lookahead (it is first used by the step's third MFMA)
+                constexpr int AH = 2, NS = 9 * MT_W;
+                constexpr int AL = (MT_W * NW * 4 <= 48 || CISTA_KPIPE >= 3) ? 2 : 1;
+                auto aaddr = [&](int st) { return abase[st % MT_W] + ((st / MT_W) / 3) * HWd + ((st / MT_W) % 3); };
+                u32x4 ah[AH + 1], al[AL + 1];
+#pragma unroll
+                for (int st = 0; st < AH; ++st) ah[st] = cur[aaddr(st)];
+#pragma unroll
+                for (int st = 0; st < AL; ++st) al[st] = cur[4 * HPpad + aaddr(st)];
+#pragma unroll
+                for (int tap = 0; tap < 9; ++tap)
+#pragma unroll
+                for (int m = 0; m < MT_W; ++m) {
+                    const int st = tap * MT_W + m;
+                    if (m == 0) {
+                        if (tap + D <= 8) {
+                            const u32x4 *wq = wp + (size_t)(tap + D) * tapstride;
+#pragma unroll
+                            for (int n = 0; n < NW; ++n) {
+                                bh[(tap + D) % (D + 1)][n] = wq[n * 128];
+                                bl[(tap + D) % (D + 1)][n] = wq[n * 128 + 64];
+                            }
+                        }
+                        if (tap == 0 && more) stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
+                    }
+                    if (st + AH < NS) ah[(st + AH) % (AH + 1)] = cur[aaddr(st + AH)];
+                    if (st + AL < NS) al[(st + AL) % (AL + 1)] = cur[4 * HPpad + aaddr(st + AL)];
+                    const f16x8 xh = __builtin_bit_cast(f16x8, ah[st % (AH + 1)]);
+                    const f16x8 xl = __builtin_bit_cast(f16x8, al[st % (AL + 1)]);
+                    const int slot = tap % (D + 1);
+#pragma unroll
+                    for (int n = 0; n < NW; ++n) {
+                        const f16x8 wh = __builtin_bit_cast(f16x8, bh[slot][n]);
+                        const f16x8 wl = __builtin_bit_cast(f16x8, bl[slot][n]);
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xh, acc[m][n], 0, 0, 0);
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wl, xh, acc[m][n], 0, 0, 0);
+                        acc[m][n] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wh, xl, acc[m][n], 0, 0, 0);
+                    }
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+            } else
+#endif
 #pragma unroll
             for (int tap = 0; tap < 9; ++tap) {
                 if (tap + D <= 8) {
