@@ -1024,18 +1024,17 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                 }
             float4 sv0[NI], sv1[NI];
 #if CISTA_KPIPE
-            if constexpr (STAGE == STAGE_S1 && EPI != EPI_PH4 && (MT_W * NW * 4 <= 48 || CISTA_KPIPE >= 2)) {
+            if constexpr (STAGE == STAGE_S1 && EPI != EPI_PH4 && MT_W * NW * 4 <= 48) {
                 // A (pixel) fragments AH = 2 (tap, m-tile) steps ahead across tap boundaries
-                // (mfma_tap reads one m-tile ahead, ~2 MFMAs before use); same products, same order.
-                // AL: the lo fragment's lookahead (it is first used by the step's third MFMA)
+                // (mfma_tap reads one m-tile ahead, ~2 MFMAs before use); same products, same order
                 constexpr int AH = 2, NS = 9 * MT_W;
-                constexpr int AL = (MT_W * NW * 4 <= 48 || CISTA_KPIPE >= 3) ? 2 : 1;
                 auto aaddr = [&](int st) { return abase[st % MT_W] + ((st / MT_W) / 3) * HWd + ((st / MT_W) % 3); };
-                u32x4 ah[AH + 1], al[AL + 1];
+                u32x4 ah[AH + 1], al[AH + 1];
 #pragma unroll
-                for (int st = 0; st < AH; ++st) ah[st] = cur[aaddr(st)];
-#pragma unroll
-                for (int st = 0; st < AL; ++st) al[st] = cur[4 * HPpad + aaddr(st)];
+                for (int st = 0; st < AH; ++st) {
+                    ah[st] = cur[aaddr(st)];
+                    al[st] = cur[4 * HPpad + aaddr(st)];
+                }
 #pragma unroll
                 for (int tap = 0; tap < 9; ++tap)
 #pragma unroll
@@ -1052,10 +1051,12 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                         }
                         if (tap == 0 && more) stage_issue_px<STAGE, NI>(a, nseg, nsegC, nchoff, spix, sg, sv0, sv1, b);
                     }
-                    if (st + AH < NS) ah[(st + AH) % (AH + 1)] = cur[aaddr(st + AH)];
-                    if (st + AL < NS) al[(st + AL) % (AL + 1)] = cur[4 * HPpad + aaddr(st + AL)];
+                    if (st + AH < NS) {
+                        ah[(st + AH) % (AH + 1)] = cur[aaddr(st + AH)];
+                        al[(st + AH) % (AH + 1)] = cur[4 * HPpad + aaddr(st + AH)];
+                    }
                     const f16x8 xh = __builtin_bit_cast(f16x8, ah[st % (AH + 1)]);
-                    const f16x8 xl = __builtin_bit_cast(f16x8, al[st % (AL + 1)]);
+                    const f16x8 xl = __builtin_bit_cast(f16x8, al[st % (AH + 1)]);
                     const int slot = tap % (D + 1);
 #pragma unroll
                     for (int n = 0; n < NW; ++n) {
