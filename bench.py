@@ -798,15 +798,36 @@ def launch_ranks(n, argv, poll_s=0.2):
     children, and as soon as one fails it stops the others (their exact PIDs) so no rank is
     left waiting in a collective.  Returns the exit code: 0 only if every rank exited 0.
     Replaces the reference's single-GPU picker (train_e2v.py:3-14, test_e2v.py:2-13)."""
+    import signal
     import subprocess
     from v2e2v_amd.dist import LAUNCHER_ENV
     port = str(_free_port())
+
+    def die_with_parent():
+        # in the child, before it runs anything: SIGTERM when the launcher dies (Linux prctl
+        # PR_SET_PDEATHSIG), so a launcher killed from outside leaves no rank holding a GPU
+        try:
+            import ctypes as _ct
+            _ct.CDLL("libc.so.6", use_errno=True).prctl(1, signal.SIGTERM)
+        except OSError:
+            pass
+
     procs = []
     for r in range(n):
         env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n), LOCAL_WORLD_SIZE=str(n),
                    MASTER_ADDR="127.0.0.1", MASTER_PORT=port)
         env[LAUNCHER_ENV] = "bench.py"
-        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv), env=env,
+                                      preexec_fn=die_with_parent))
+
+    def forward(signum, _frame):            # a terminated launcher stops its ranks first
+        for p in procs:
+            if p.poll() is None:
+                p.send_signal(signum)
+        raise SystemExit(128 + signum)
+
+    for sig in (signal.SIGTERM, signal.SIGINT):
+        signal.signal(sig, forward)
     rc = 0
     try:
         while [p.poll() for p in procs].count(None):

@@ -82,3 +82,29 @@ def test_rank_plan(monkeypatch):
     monkeypatch.setenv("WORLD_SIZE", "1")
     with pytest.raises(SystemExit):
         bench.rank_plan(ns(8))                                    # torchrun N=1 with --gpus 8
+
+
+def test_terminated_launcher_stops_its_ranks():
+    """SIGTERM to the launching process reaches every rank (forwarded, and PR_SET_PDEATHSIG if the
+    launcher dies outright): no rank is left running -- on the GPU box, holding a GPU."""
+    import signal
+    import time
+    psutil = pytest.importorskip("psutil")
+    p = subprocess.Popen([sys.executable, BENCH, "--gpus", "2", "--dry-run", "--steps", "400000000"],
+                         env=_env(), cwd=ROOT, stdout=subprocess.DEVNULL, stderr=subprocess.DEVNULL)
+    try:
+        kids = []
+        for _ in range(120):                          # the ranks are up once both are children
+            kids = psutil.Process(p.pid).children()
+            if len(kids) == 2:
+                break
+            time.sleep(0.25)
+        assert len(kids) == 2
+        time.sleep(2.0)
+        p.send_signal(signal.SIGTERM)
+        assert p.wait(timeout=60) != 0
+        gone, alive = psutil.wait_procs(kids, timeout=60)
+        assert not alive
+    finally:
+        if p.poll() is None:
+            p.kill()
