@@ -194,13 +194,6 @@ int cista_launch_layer(const cista_config *cfg, const void *packed, int layer, i
  * reads), 0: row-major m-tiles.  Host-only (no device call); introspection for tests, not a
  * reference interface. */
 int cista_tile_plan(int B, int Hout, int Wout, int block_px, int *out);
-/* Two-tile ISTA convs (cista_pingpong.hpp): the inference ISTA D / P launches of base_channels 64
- * at >= 16 tiles per CU run as persistent 512-thread workgroups whose two halves alternate their
- * K loops and memory phases.  Bit-identical to the one-tile kernel.  enable = a mask (bit 0 ISTA
- * D, bit 1 ISTA P) of where the process uses them (initially CISTA_PP from the environment, else
- * 3); < 0 only queries; returns the previous mask.  Host-only; for tests and same-process A/B
- * timing, not a reference interface. */
-int cista_set_two_tile(int enable);
 
 /* ---- training: BPTT backward (reference train_e2v.py:108-130
  * differentiates through the whole recurrent sequence with autograd) ----

@@ -93,7 +93,6 @@ def _declare(lib):
         "cista_layer_macs": (ctypes.c_double, [P(CistaConfig), c_int, c_int, c_int, c_int]),
         "cista_layer_fused": (c_int, [P(CistaConfig), c_int]),
         "cista_tile_plan": (c_int, [c_int, c_int, c_int, c_int, P(c_int)]),
-        "cista_set_two_tile": (c_int, [c_int]),
         "cista_saved_bytes": (c_size_t, [P(CistaConfig), c_int, c_int, c_int]),
         "cista_train_workspace_bytes": (c_size_t, [P(CistaConfig), c_int, c_int, c_int]),
         "cista_forward_train": (c_int, [P(CistaConfig), c_void_p, c_int, c_int, c_int, P(CistaFrameIO),

@@ -6,13 +6,11 @@
 #include <stdlib.h>
 #include <string.h>
 
-#include <atomic>
 #include <mutex>
 
 #include "../../include/cista_lstc.h"
 #include "cista_kernels.hpp"
 #include "cista_backward.hpp"
-#include "cista_pingpong.hpp"
 
 using namespace cista;
 
@@ -112,8 +110,6 @@ struct Workspace {
     float *x1;     // (B,h,w,C)
     float *z0;     // (B,h,w,2C)
     float *xb;     // (B,h,w,C): ISTA x = x1 - D(z); later Dg output y
-    PPOverflow *ovf;   // overflow list of the two-tile ISTA convs (capacity ovf_cap items)
-    int ovf_cap;
     size_t bytes;
 };
 
@@ -130,9 +126,6 @@ Workspace carve(void *ws, int B, int H, int W, int C) {
     w.x1 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * C * 4);
     w.z0 = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * 2 * C * 4);
     w.xb = reinterpret_cast<float *>(base + off); off = align_up(off + (size_t)B * hw * C * 4);
-    // every tile of a two-tile launch covers >= 16 output pixels (launch_conv_pp checks the count)
-    w.ovf_cap = (int)((size_t)B * hw / 16 + 256);
-    w.ovf = reinterpret_cast<PPOverflow *>(base + off); off = align_up(off + 256 + (size_t)w.ovf_cap * 4);
     w.bytes = off;
     return w;
 }
@@ -454,85 +447,6 @@ int launch_conv(const ConvArgs &a, hipStream_t st) {
     }
 }
 
-// compute units of the current device (the persistent two-tile grid: one workgroup per CU)
-int device_cus() {
-    static std::mutex mu;
-    static int cus[64] = {0};
-    int dev = 0;
-    if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) return 0;
-    std::lock_guard<std::mutex> lock(mu);
-    if (!cus[dev] && hipDeviceGetAttribute(&cus[dev], hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-        cus[dev] = 0;
-    return cus[dev];
-}
-
-// bit 0: ISTA D, bit 1: ISTA P; -1: not yet read from the environment (CISTA_PP, default 0:
-// measured slower)
-std::atomic<int> g_two_tile{-1};
-int pp_mask() {
-    int v = g_two_tile.load(std::memory_order_relaxed);
-    if (v < 0) {
-        const char *e = getenv("CISTA_PP");
-        int expect = -1;
-        g_two_tile.compare_exchange_strong(expect, e ? (atoi(e) & 3) : 0);
-        v = g_two_tile.load(std::memory_order_relaxed);
-    }
-    return v;
-}
-
-// The two-tile persistent ISTA convs (cista_pingpong.hpp) for the inference forward: the same
-// tiling as launch_conv_cfg<MT_W, NW, WM, WN, STAGE_S1, EPI, 1, true, 4> (so the same per-pixel
-// arithmetic), one 512-thread workgroup per CU.  Returns 1 (not launched) where it does not
-// apply: too few items for the persistent halves to pipeline (below 8 tiles per half-slot), or
-// geometry beyond the kernel's limits.
-template <int MT_W, int NW, int WM, int WN, int EPI>
-int launch_conv_pp(ConvArgs a, PPOverflow *ovf, int ovf_cap, hipStream_t st) {
-    constexpr int block_px = WM * MT_W * 16, nblk_cols = WN * NW * 16;
-    if (!(pp_mask() & (EPI == EPI_ISTA_P ? 2 : 1)) || !ovf || a.in1 || a.out1 || a.out2 || a.N % nblk_cols || a.c0 % 32) return 1;
-    const int ncu = device_cus();
-    if (ncu < 8) return 1;
-    const TilePlan plan = plan_tiles(a.B, a.Hout, a.Wout, block_px, 1, 4 * 256, 2, 2, true, 0.0);
-    const long tiles = (long)plan.a.ty * plan.a.tx + (long)plan.b.ty * plan.b.tx;
-    const long items = (long)a.B * tiles * (a.N / nblk_cols);
-    if (items < 16L * ncu || items > ovf_cap) return 1;
-    if ((long long)a.B * a.Hout * a.Wout * a.Cout >= (1LL << 31) || (long long)a.B * a.Hin * a.Win * a.c0 >= (1LL << 31))
-        return 1;
-    a.ox_base = 0;
-    a.TH = plan.a.TH; a.TW = plan.a.TW;
-    a.pitch = plan.a.mseg ? 16 * plan.a.mseg : plan.a.TW;
-    a.rcp_pitch = 1.0f / (float)a.pitch;
-    a.tiles_y = plan.a.ty; a.tiles_x = plan.a.tx;
-    a.tiles_x_b = plan.b.tx; a.tiles_y_b = plan.b.ty;
-    a.TH_b = plan.b.TH; a.TW_b = plan.b.TW;
-    a.pitch_b = plan.b.mseg ? 16 * plan.b.mseg : plan.b.TW;
-    a.rcp_pitch_b = plan.b.tx ? 1.0f / (float)a.pitch_b : 0.0f;
-    a.wa = plan.wa;
-    PingPongArgs p;
-    p.a = a;
-    p.items = (int)items;
-    p.items_a = (int)((long)a.B * plan.a.ty * plan.a.tx * (a.N / nblk_cols));
-    const size_t img = plan.b.lds > plan.a.lds ? plan.b.lds / 2 : plan.a.lds / 2;   // Tile.lds: 2 images
-    p.img_u4 = (int)(img / 16);
-    p.overflow = ovf;
-    const size_t lds = 4 * img + 64;
-    if (lds > 160 * 1024) return 1;
-    auto kern = conv3x3_pingpong<MT_W, NW, WM, WN, EPI>;
-    if (!allow_big_lds((const void *)kern)) return CISTA_ERR_HIP;
-    // the fixup kernel runs conv_tile: its LDS (two images, or the epilogue's table + range-pass
-    // scratch) as launch_conv_cfg sizes it
-    const size_t epi_lds = (size_t)MT_W * WM * 16 * 4 > (size_t)9 * a.Cout * 4 ? (size_t)MT_W * WM * 16 * 4
-                                                                                : (size_t)9 * a.Cout * 4;
-    p.a.lds_flag = (int)(epi_lds / 4);
-    const size_t flds = 2 * img > epi_lds + 12 * 4 ? 2 * img : epi_lds + 12 * 4;
-    auto fix = conv3x3_fixup<MT_W, NW, WM, WN, EPI>;
-    if (!allow_big_lds((const void *)fix)) return CISTA_ERR_HIP;
-    const long nwg = items / 2 < ncu ? items / 2 : ncu;
-    if (hipMemsetAsync(ovf, 0, sizeof(unsigned), st) != hipSuccess) return CISTA_ERR_HIP;
-    hipLaunchKernelGGL(kern, dim3((unsigned)nwg), dim3(512), lds, st, p);
-    hipLaunchKernelGGL(fix, dim3(64), dim3(WM * WN * 64), flds, st, p);
-    return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
-}
-
 ConvArgs conv_args(const void *packed, const Layout &L, int id, int C, int B, int Hin, int Win,
                    int Hout, int Wout, const float *in0, int c0, const float *in1, int c1) {
     ConvArgs a;
@@ -583,8 +497,6 @@ struct Frame {
     float *z;       // LSTC output, then ISTA iterate (in place)       (B,h,w,2C)
     float *hs, *cs; // ConvLSTM state                                  (B,h,w,C)
     float *rec, *pre;
-    PPOverflow *ovf;       // overflow list of the two-tile ISTA convs (NULL: not available)
-    int ovf_cap;
     // training forward: activations saved for the backward (all NULL at inference)
     float *gi, *gf, *go;   // ConvLSTC gates (sigmoid)                    (B,h,w,2C) each
     float *zl;             // depth x ISTA z_k, z_0 = ConvLSTC output      (B,h,w,2C)
@@ -769,10 +681,6 @@ int run_layer(const Frame &f, int layer, int it = 0) {
         case CISTA_LAYER_ISTA_D:    // x = x1 - D(z)                              e2v_model.py:73-74
             a = conv_args_f(f, CV_D, C, B, h, w, h, w, z_in, 2 * C, nullptr, 0);
             a.out0 = f.xs ? f.xs + it * hw * C : f.xb; a.aux0 = f.x1;
-            if (C == 64 && !f.xs) {
-                const int pp = launch_conv_pp<6, 2, 2, 2, EPI_ISTA_D>(a, f.ovf, f.ovf_cap, f.st);
-                if (pp != 1) return pp;
-            }
             return launch_conv<STAGE_S1, EPI_ISTA_D, 1>(a, f.st);
         case CISTA_LAYER_ISTA_P:    // z = softshrink(P(x) + z, lambda)            :75-77
             a = conv_args_f(f, CV_P, C, B, h, w, h, w, f.xs ? f.xs + it * hw * C : f.xb, C,
@@ -785,10 +693,6 @@ int run_layer(const Frame &f, int layer, int it = 0) {
                 return launch_conv<STAGE_S1, EPI_ISTA_P_L2, 1>(a, f.st);
             }
 #endif
-            if (C == 64 && !f.v) {
-                const int pp = launch_conv_pp<12, 2, 1, 4, EPI_ISTA_P>(a, f.ovf, f.ovf_cap, f.st);
-                if (pp != 1) return pp;
-            }
             return launch_conv<STAGE_S1, EPI_ISTA_P, 1>(a, f.st);
         case CISTA_LAYER_DG:        // y = relu(Dg.conv(z))                      base_layers.py:222
             a = conv_args_f(f, CV_DG, C, B, h, w, h, w, f.z, 2 * C, nullptr, 0);
@@ -862,7 +766,6 @@ Frame make_frame(const cista_config *cfg, const void *packed, int B, int H, int 
     f.B = B; f.H = H; f.W = W; f.h = H / 2; f.w = W / 2; f.C = cfg->base_channels;
     const Workspace wsp = carve(ws, B, H, W, f.C);
     f.full = wsp.full; f.x1 = wsp.x1; f.z0 = wsp.z0; f.xb = wsp.xb;
-    f.ovf = wsp.ovf; f.ovf_cap = wsp.ovf_cap;
     f.st = static_cast<hipStream_t>(stream);
     return f;
 }
@@ -1933,12 +1836,6 @@ int cista_tile_plan(int B, int Hout, int Wout, int block_px, int *out) {
     out[12] = one.mseg;
     out[13] = 0;
     return CISTA_OK;
-}
-
-int cista_set_two_tile(int enable) {
-    const int prev = pp_mask();
-    if (enable >= 0) g_two_tile.store(enable & 3, std::memory_order_relaxed);
-    return prev;
 }
 
 int cista_layer_fused(const cista_config *cfg, int layer) {
