@@ -81,3 +81,32 @@ def test_graph_replay_two_region_batch_bit_identical():
         one, ost = eager(m, vox[:, s:s + 1].contiguous(), torch.zeros(1, 1, H, W, device=DEV), None)
         assert torch.equal(recs[:, s:s + 1], one)
         assert torch.equal(st[1][s:s + 1], ost[1]) and torch.equal(st[2][1][s:s + 1], ost[2][1])
+
+
+def test_bench_configuration_graph_replay_against_cpu_restatement():
+    """The headline's timed configuration itself (bench.py: config c2, 180x240, 5 bins, depth 5,
+    C=64, B=256 sequences, whole-sequence graph replay with the two-region tiling and XCD item
+    order), 3 recurrent frames: the first and last sequences of the batch against the reference's
+    forward restated on ATen's CPU kernels (oracle/cista_oracle_torch.py; pinned to the golden
+    vectors), every pixel within 1e-4 of itself, states within 1e-4 of their max.
+    Reference semantics: test_e2v.py:105-117 (prev_image = previous output, states carried)."""
+    import bench
+    from tests.conftest import elem_rel_err, rel_err
+    from oracle.cista_oracle_torch import CistaLSTCTorchCPU
+    B, H, W, L = 256, 180, 240, 3
+    m = CistaLSTCNet([H, W])
+    bench.he_init_(torch, m, seed=7)                      # the bench's own weights
+    m = m.to(DEV).eval()
+    vox = bench.synth_voxels(torch, L, B, 5, H, W, 15000, seed=1000, device=torch.device(DEV))
+    seq = CistaSequence(m, vox)
+    recs, st = seq.run()
+    torch.cuda.synchronize()
+    sd = {k: v.detach().cpu().numpy() for k, v in m.state_dict().items()}
+    ref = CistaLSTCTorchCPU(fx.collapse_tied(sd, 5), 5)
+    for s in (0, B - 1):
+        o_recs, o_st = ref.run_sequence(vox[:, s:s + 1].cpu().numpy())
+        assert elem_rel_err(recs[:, s:s + 1].cpu().numpy(), o_recs) < 1e-4
+        got = [st[0][s:s + 1], st[1][s:s + 1], st[2][0][s:s + 1], st[2][1][s:s + 1]]
+        for g, r in zip(got, [o_st[0], o_st[1], o_st[2][0], o_st[2][1]]):
+            assert rel_err(g.cpu().numpy(), r) < 1e-4
+    seq.close()
