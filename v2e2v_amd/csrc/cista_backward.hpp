@@ -827,6 +827,27 @@ __device__ unsigned long long *g_cista_wstamps;
 #define WT_STAMP(slot, v) do { } while (0)
 #endif
 
+#ifndef CISTA_WT_XCD
+#define CISTA_WT_XCD 1    // XCD-contiguous (block, split) order (0: blockIdx order, A/B builds)
+#endif
+// (channel block, split) of this workgroup.  Workgroups are dispatched to the 8 XCDs round-robin
+// by linear id, so in blockIdx order the channel blocks of one split -- which stage the same X
+// tiles at the same time -- sit on different XCDs and each fetches X from HBM.  Renumbering the
+// workgroups so that every XCD holds a contiguous run of (split, block) puts them, and the
+// neighbouring splits whose halos overlap, behind one L2.  Each split computes the same tiles
+// either way (results unchanged).
+__device__ __forceinline__ void wt_block_split(int &blk, int &split) {
+    const int n = gridDim.x * gridDim.y, l = blockIdx.y * gridDim.x + blockIdx.x;
+#if CISTA_WT_XCD
+    const int xcd = l & 7, per = n >> 3, rem = n & 7;
+    const int q = xcd * per + (xcd < rem ? xcd : rem) + (l >> 3);
+#else
+    const int q = l;
+#endif
+    blk = q % gridDim.x;
+    split = q / gridDim.x;
+}
+
 template <int XS>
 __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs a) {
     using GE = WtGeo<XS>;
@@ -837,7 +858,9 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     int *xfl = reinterpret_cast<int *>(xmx + 4);                 // [2][4] per-buffer overflow flags
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int ncb = (a.Cin + 63) / 64;
-    const int co0 = (blockIdx.x / ncb) * 64, ci0 = (blockIdx.x % ncb) * 64;
+    int blk, split;
+    wt_block_split(blk, split);
+    const int co0 = (blk / ncb) * 64, ci0 = (blk % ncb) * 64;
     const bool loader = wave >= WT_NMW;        // waves 0 .. NMW-1: MFMAs; the last 4: staging
     const int ntiles = a.B * a.tiles_y * a.tiles_x;
     const float gsc = a.gscale[0];
@@ -850,7 +873,7 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     // ---- staging (loader waves): item (pixel 4 set + sp, channel quad sq of plane sb) ----
     const int lw = wave - WT_NMW;
     const int sb = lane >> 4, sp = (lane >> 2) & 3, sq = lane & 3;
-    const bool do_bias = a.bpartial && (blockIdx.x % ncb) == 0;
+    const bool do_bias = a.bpartial && (blk % ncb) == 0;
     float4 bsum = make_float4(0.f, 0.f, 0.f, 0.f);
     float4 gv[GE::UG], xv[GE::UX];
     auto tile_origin = [&](int tile, int &b, int &oy0, int &ox0) __attribute__((always_inline)) {
@@ -957,16 +980,16 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
         if (__builtin_amdgcn_readfirstlane(threadIdx.x) >= 64 * WT_NMW) __builtin_amdgcn_s_setprio(CISTA_WT_PRIO);
 #endif
         WT_STAMP(0, __builtin_amdgcn_s_memtime());
-        if ((int)blockIdx.y < ntiles) {
-            load_tile(blockIdx.y);
+        if (split < ntiles) {
+            load_tile(split);
             commit(sm, xfl);
             WT_STAMP(1, __builtin_amdgcn_s_memtime());
-            if ((int)blockIdx.y + a.nsplit < ntiles) load_tile(blockIdx.y + a.nsplit);
+            if (split + a.nsplit < ntiles) load_tile(split + a.nsplit);
         }
         __syncthreads();
         WT_STAMP(2, __builtin_amdgcn_s_memtime());
         int it = 0;
-        for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
+        for (int tile = split; tile < ntiles; tile += a.nsplit, ++it) {
             const int bi = it & 1;
             if (__builtin_expect(flagged(bi), 0)) {
                 __syncthreads();
@@ -1014,7 +1037,7 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
     __syncthreads();
     WT_STAMP(1, __builtin_amdgcn_s_memtime());
     int it = 0;
-    for (int tile = blockIdx.y; tile < ntiles; tile += a.nsplit, ++it) {
+    for (int tile = split; tile < ntiles; tile += a.nsplit, ++it) {
         const int bi = it & 1;
         // the tile's X scale: from its own maximum when flagged, else 1 (powers of two, so the
         // accumulator rescale by r is exact)
@@ -1092,12 +1115,12 @@ __global__ __launch_bounds__(WT_THREADS, 1) void wgrad_tr_kernel(const WgradArgs
             float t = 0.0f;
             for (int w = 0; w < 4; ++w)
                 for (int p = 0; p < 4; ++p) t += (&red[64 * w + 16 * b16 + 4 * p + q4].x)[e];
-            a.bpartial[(size_t)blockIdx.y * a.Cout + co0 + tid] = t;
+            a.bpartial[(size_t)split * a.Cout + co0 + tid] = t;
         }
     }
     // acc[u][v][t][j]: row (cout) 16 (pco + u) + 4 (lane >> 4) + j, col (cin) 16 (pci + v) + (lane & 15)
     const float inv = a.gscale[1] * (1.0f / sx);
-    float *part = a.partial + (size_t)blockIdx.y * a.Cout * a.Cin * 9;
+    float *part = a.partial + (size_t)split * a.Cout * a.Cin * 9;
 #pragma unroll
     for (int v = 0; v < NV; ++v) {
         const int ci = ci0 + 16 * (pci + v) + (lane & 15);
