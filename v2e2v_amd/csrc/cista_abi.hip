@@ -304,6 +304,21 @@ double zp2_halo_weight() {
     return w;
 }
 
+#if CISTA_STAMPS
+// diagnostic builds only (scripts/dgrad_stamps.py): every EPI_FOLD launch after
+// cista_debug_set_fold_stamps stamps into a region of its own, FOLD_STAMP_WG workgroups x 4
+// waves x 24 slots, in launch order, until the ring is full
+constexpr size_t FOLD_STAMP_WG = 2048;
+std::mutex g_fold_mu;
+unsigned long long *g_fold_ring = nullptr;
+int g_fold_cap = 0, g_fold_next = 0;
+unsigned long long *fold_stamp_region(unsigned nwg) {
+    std::lock_guard<std::mutex> lock(g_fold_mu);
+    if (!g_fold_ring || g_fold_next >= g_fold_cap || nwg > FOLD_STAMP_WG) return nullptr;
+    return g_fold_ring + (size_t)(g_fold_next++) * FOLD_STAMP_WG * 4 * 24;
+}
+#endif
+
 template <int MT_W, int NW, int WM, int WN, int STAGE, int EPI, int G, bool PF = false, int NI = 0, int OCC = 2>
 int launch_conv_cfg(ConvArgs a, hipStream_t st) {
     constexpr int block_px = WM * MT_W * 16;
@@ -375,6 +390,10 @@ int launch_conv_cfg(ConvArgs a, hipStream_t st) {
 #endif
     const size_t tlds = plan.b.lds > plan.a.lds ? plan.b.lds : plan.a.lds;
     const size_t lds = tlds > epi_lds + 12 * NWV ? tlds : epi_lds + 12 * NWV;
+#if CISTA_STAMPS
+    a.stamps = nullptr;
+    if constexpr (EPI == EPI_FOLD) a.stamps = fold_stamp_region(grid.x * grid.y);
+#endif
     hipLaunchKernelGGL(kern, grid, dim3(NT), lds, st, a);
     if (hipGetLastError() != hipSuccess) return CISTA_ERR_HIP;
     return CISTA_OK;
@@ -1536,6 +1555,16 @@ int cista_debug_set_ista_p_probe(unsigned mask) {
 int cista_debug_set_stamps(void *buf) {
     return hipMemcpyToSymbol(HIP_SYMBOL(cista::g_cista_stamps), &buf, sizeof(buf)) == hipSuccess ? CISTA_OK
                                                                                             : CISTA_ERR_HIP;
+}
+// ... per EPI_FOLD launch, nlaunch regions of FOLD_STAMP_WG x 96 words (NULL: off); returns
+// the number of regions filled since the previous call
+int cista_debug_set_fold_stamps(void *buf, int nlaunch) {
+    std::lock_guard<std::mutex> lock(g_fold_mu);
+    const int used = g_fold_next;
+    g_fold_ring = static_cast<unsigned long long *>(buf);
+    g_fold_cap = buf ? nlaunch : 0;
+    g_fold_next = 0;
+    return used;
 }
 // ... and wgrad_tr_kernel's (scripts/wgrad_stamps.py)
 int cista_debug_set_wstamps(void *buf) {

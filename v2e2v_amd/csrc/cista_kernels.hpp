@@ -58,6 +58,9 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_KPIPE
 #define CISTA_KPIPE 1
 #endif
+#ifndef CISTA_PRE2
+#define CISTA_PRE2 1      // two-chunk convs stage both K-chunks in the prologue (0: A/B builds)
+#endif
 // Diagnostic build only (CISTA_STAMPS=1, scripts/stamps.py): lane 0 of every conv wave records
 // shader-clock timestamps of its phases into g_cista_stamps[(block * 4 + wave) * 24 + slot]:
 // 0 hw id | xcc << 32, 1 start, 2 prologue staged, 3 + k end of K-chunk k (k < 8), 11 MFMA loop
@@ -71,7 +74,7 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 __device__ unsigned long long *g_cista_stamps;
 #define CISTA_STAMP(slot, v)                                                                    \
     do {                                                                                         \
-        unsigned long long *_p = g_cista_stamps;                                                 \
+        unsigned long long *_p = a.stamps ? a.stamps : g_cista_stamps;                           \
         if (_p && (threadIdx.x & 63) == 0) _p[(blockIdx.x * 4 + (threadIdx.x >> 6)) * 24 + (slot)] = (v); \
     } while (0)
 #else
@@ -187,6 +190,9 @@ struct ConvArgs {
     int ox_base;
     int TH_b, TW_b, tiles_x_b, tiles_y_b, pitch_b, wa;
     float rcp_pitch_b;
+#if CISTA_STAMPS
+    unsigned long long *stamps;   // diagnostic builds: this launch's stamp region (NULL: g_cista_stamps)
+#endif
 };
 
 // floor(n / d) for 0 <= n < 2048 and 1 <= d <= 512 through fp32, given rcp_d = 1 / d correctly
@@ -991,17 +997,30 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                       "double-buffered staging: direct (reflect / zero / edge padded) inputs");
         int spix[NI], shp[NI], sg[NI];
         stage_pixels<STAGE, NI, NTH>(a, b, iy0, ix0, HH, HWd, spix, shp, sg, tid);
+        // two K-chunks (Cin = 64): both are staged here, their halo round trips in flight
+        // together, and the K loop issues no halo loads.  (A chunk's halo loads issued inside
+        // the loop hold up the first B-fragment wait behind them -- vmcnt completes in order --
+        // and stalled chunk 0 by about one HBM round trip.)
+        const bool pre2 = CISTA_PRE2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2) && nchunks == 2;
         {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
             float4 sv0[NI], sv1[NI];
             stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, sv0, sv1, b);
-            stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
+            if (pre2) {
+                float4 tv0[NI], tv1[NI];
+                seg_of(1, seg, segC, choff);
+                stage_issue_px<STAGE, NI>(a, seg, segC, choff, spix, sg, tv0, tv1, b);
+                stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
+                stage_commit<NI>(smem + 8 * HPpad, HPpad, tv0, tv1, shp, sg, amax);
+            } else {
+                stage_commit<NI>(smem, HPpad, sv0, sv1, shp, sg, amax);
+            }
         }
         __syncthreads();
         CISTA_STAMP(2, __builtin_amdgcn_s_memtime());
         for (int kc = 0; kc < nchunks; ++kc) {
-            const bool more = kc + 1 < nchunks;
+            const bool more = !pre2 && kc + 1 < nchunks;
             const u32x4 *cur = smem + (kc & 1) * 8 * HPpad;
             u32x4 *nxt = smem + ((kc + 1) & 1) * 8 * HPpad;
             const float *nseg; int nsegC, nchoff;
@@ -1086,7 +1105,7 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
                     mfma_tap<MT_W, NW>(acc, cur, abase, (tap / 3) * HWd + (tap % 3), HPpad, bh[slot], bl[slot]);
             }
             if (more) stage_commit<NI>(nxt, HPpad, sv0, sv1, shp, sg, amax);
-            __syncthreads();
+            if (!pre2 || kc + 1 == nchunks) __syncthreads();   // pre-staged: nothing to publish mid-loop
             if (kc < 8) CISTA_STAMP(3 + kc, __builtin_amdgcn_s_memtime());
         }
     } else {
@@ -1290,6 +1309,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
 #pragma unroll
             for (int n = 0; n < NW; ++n) acc[m][n] *= ws;   // exact: power of two
         conv_fold_epilogue<MT_W, NW, WM, NWV>(a, smem, acc, b, oy0, ox0, wm, nt0);
+        CISTA_STAMP(12, __builtin_amdgcn_s_memtime());
+        CISTA_STAMP(14, __builtin_amdgcn_s_memrealtime());
         return;
     }
 
