@@ -827,23 +827,17 @@ __device__ unsigned long long *g_cista_wstamps;
 #define WT_STAMP(slot, v) do { } while (0)
 #endif
 
-#ifndef CISTA_WT_XCD
-#define CISTA_WT_XCD 1    // XCD-contiguous (block, split) order (0: blockIdx order, A/B builds)
-#endif
 // (channel block, split) of this workgroup.  Workgroups are dispatched to the 8 XCDs round-robin
 // by linear id, so in blockIdx order the channel blocks of one split -- which stage the same X
 // tiles at the same time -- sit on different XCDs and each fetches X from HBM.  Renumbering the
 // workgroups so that every XCD holds a contiguous run of (split, block) puts them, and the
-// neighbouring splits whose halos overlap, behind one L2.  Each split computes the same tiles
-// either way (results unchanged).
+// neighbouring splits whose halos overlap, behind one L2 (stacked ISTA P wgrad: 551 -> 428 MB per
+// launch, time unchanged; the blockIdx-order arm is in commit 8ce774e).  Each split computes the
+// same tiles either way (results unchanged).
 __device__ __forceinline__ void wt_block_split(int &blk, int &split) {
     const int n = gridDim.x * gridDim.y, l = blockIdx.y * gridDim.x + blockIdx.x;
-#if CISTA_WT_XCD
     const int xcd = l & 7, per = n >> 3, rem = n & 7;
     const int q = xcd * per + (xcd < rem ? xcd : rem) + (l >> 3);
-#else
-    const int q = l;
-#endif
     blk = q % gridDim.x;
     split = q / gridDim.x;
 }

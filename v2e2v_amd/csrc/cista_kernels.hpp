@@ -58,9 +58,6 @@ typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 #ifndef CISTA_KPIPE
 #define CISTA_KPIPE 1
 #endif
-#ifndef CISTA_PRE2
-#define CISTA_PRE2 1      // two-chunk convs stage both K-chunks in the prologue (0: A/B builds)
-#endif
 // Diagnostic build only (CISTA_STAMPS=1, scripts/stamps.py): lane 0 of every conv wave records
 // shader-clock timestamps of its phases into g_cista_stamps[(block * 4 + wave) * 24 + slot]:
 // 0 hw id | xcc << 32, 1 start, 2 prologue staged, 3 + k end of K-chunk k (k < 8), 11 MFMA loop
@@ -1000,8 +997,8 @@ __device__ __forceinline__ void conv_tile(const ConvArgs &a, u32x4 *smem, unsign
         // two K-chunks (Cin = 64): both are staged here, their halo round trips in flight
         // together, and the K loop issues no halo loads.  (A chunk's halo loads issued inside
         // the loop hold up the first B-fragment wait behind them -- vmcnt completes in order --
-        // and stalled chunk 0 by about one HBM round trip.)
-        const bool pre2 = CISTA_PRE2 && (STAGE == STAGE_S1 || STAGE == STAGE_ZP2) && nchunks == 2;
+        // and stalled chunk 0 by about one HBM round trip; the A/B arm is in commit 2d1db52.)
+        const bool pre2 = (STAGE == STAGE_S1 || STAGE == STAGE_ZP2) && nchunks == 2;
         {
             const float *seg; int segC, choff;
             seg_of(0, seg, segC, choff);
