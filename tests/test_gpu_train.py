@@ -426,3 +426,40 @@ def test_training_two_region_tiling_equals_single():
             rel_err(pi.grad[i:i + 1].cpu().numpy(), pii.grad.cpu().numpy())
         print(f"sample {i}: events grad {e1:.2e}, prev-image grad {e2:.2e}")
         assert e1 < 1e-5 and e2 < 1e-5, (i, e1, e2)
+
+
+def test_side_stream_wgrads_bit_identical(monkeypatch):
+    """The backward's weight gradients run on a side stream beside the dgrad chain
+    (cista_abi.hip on_side / join_side).  They are the same kernels on the same inputs, so a BPTT
+    step at config c3's shape (180x240, B=8, 3 frames) gives bit-identical parameter and input
+    gradients with the side stream on and off (CISTA_BWD_SIDE, read per call); a missed
+    write-after-read hazard between the two streams would show up here as a differing value."""
+    B, L = 8, 3
+    m = CistaLSTCNet([180, 240], base_channels=64, depth=5, num_bins=5)
+    params = fx.stress_params(64, 5, 5, seed=43, lam=0.05)
+    sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, 5)
+    m.load_state_dict(sd, strict=True)
+    m = m.to(DEV)
+    rng = np.random.default_rng(9)
+    vox = rng.standard_normal((L, B, 5, 180, 240)).astype(np.float32)
+    target = gpu(rng.random((B, 1, 180, 240)).astype(np.float32))
+
+    def step(side):
+        monkeypatch.setenv("CISTA_BWD_SIDE", "1" if side else "0")
+        m.zero_grad(set_to_none=True)
+        evs = [gpu(vox[f], True) for f in range(L)]
+        prev, state = torch.zeros(B, 1, 180, 240, device=DEV), None
+        for f in range(L):
+            out, state = m(evs[f], prev, state)
+            prev = out.clone()
+        (out - target).abs().mean().backward()
+        torch.cuda.synchronize()
+        return grads_by_name(m), [e.grad.detach().cpu().numpy() for e in evs]
+
+    g0, e0 = step(False)
+    g1, e1 = step(True)
+    g2, e2 = step(True)                                  # and repeatable
+    for k in g0:
+        assert np.array_equal(g0[k], g1[k]) and np.array_equal(g1[k], g2[k]), k
+    for f in range(L):
+        assert np.array_equal(e0[f], e1[f]) and np.array_equal(e1[f], e2[f]), f

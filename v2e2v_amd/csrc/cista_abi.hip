@@ -878,6 +878,7 @@ struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *gx1, *Go, *gz0;
     float *fb;          // border lines of an EPI_FOLD dgrad's padded output (fold_border_index)
     float *part, *bpart, *dlp;
+    float *part2, *bpart2;   // the side stream's wgrad partials (run_backward, on_side)
     float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
     unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses)
     float *scl;         // [16] scale pairs
@@ -918,6 +919,8 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     s.part = take((size_t)WG_BLOCKS * 32 * 32 * 9);
     s.bpart = take((size_t)WG_BLOCKS * 4 * C);
     s.dlp = take((size_t)2 * C * 512);
+    s.part2 = take((size_t)WG_BLOCKS * 32 * 32 * 9);
+    s.bpart2 = take((size_t)WG_BLOCKS * 4 * C);
     s.wT = take((size_t)9 * C * C);
     s.amax = reinterpret_cast<unsigned *>(take((size_t)8 * AMAX_SLOTS * AMAX_STRIDE));
     s.scl = take(2 * SCL_PAIRS + 4 * nd + 4);   // the call's pairs, the ISTA P / D pairs per iteration, their minima
@@ -959,9 +962,73 @@ struct Bwd {
     BwdWs ws;
     int slot;   // |max| slot set (rotating over 8)
     int pair;   // next scale pair of the call (never reused within a call)
+    hipStream_t side = nullptr;   // weight gradients' stream (NULL: everything on st)
+    bool side_busy = false;       // side work not yet joined into st
+    int dev = 0, nev = 0;         // device, events used by the call
 };
 
 int hip_ok() { return hipGetLastError() == hipSuccess ? CISTA_OK : CISTA_ERR_HIP; }
+
+// Weight gradients on a side stream.  Each wgrad of the backward reads gradients and activations
+// that are final when it is issued, so it can run beside the dgrad chain: its workgroups fill the
+// matrix pipes while the chain's one-round dgrad launches are in their memory phases
+// and while the chain's small elementwise and scale kernels hold a few CUs.  Fork: an event on the
+// caller's stream after the wgrad's inputs, waited on by the side stream; the side wgrads use their
+// own partial buffers (part2 / bpart2).  Join: before the caller's stream overwrites an input a
+// pending side wgrad reads, and at the end of the call (the caller reads the weight gradients on
+// its stream).  One side stream per device, created on first use; events from a per-thread pool
+// (a wait is bound to the event's record at the time of the call, so reuse is safe).
+// CISTA_BWD_SIDE=0 (read per call) keeps everything on the caller's stream: the same kernels in
+// the same order, so the gradients are bit-identical either way (tests/test_gpu_train.py).
+bool side_enabled() {
+    const char *e = getenv("CISTA_BWD_SIDE");
+    return !e || atoi(e) != 0;
+}
+constexpr int MAX_DEV = 64, BWD_EVENTS = 16;
+hipStream_t side_stream(int dev) {
+    static std::mutex mu;
+    static hipStream_t streams[MAX_DEV] = {};
+    if (dev < 0 || dev >= MAX_DEV) return nullptr;
+    std::lock_guard<std::mutex> lock(mu);
+    if (!streams[dev] && hipStreamCreateWithFlags(&streams[dev], hipStreamNonBlocking) != hipSuccess)
+        streams[dev] = nullptr;
+    return streams[dev];
+}
+// an event recorded on `on` now (NULL on failure)
+hipEvent_t mark(Bwd &k, hipStream_t on) {
+    thread_local hipEvent_t pool[MAX_DEV][BWD_EVENTS] = {};
+    if (k.dev < 0 || k.dev >= MAX_DEV || k.nev >= BWD_EVENTS) return nullptr;
+    hipEvent_t &e = pool[k.dev][k.nev++];
+    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
+    return e && hipEventRecord(e, on) == hipSuccess ? e : nullptr;
+}
+// `waiter` waits for the work issued to `on` so far
+int stream_wait(Bwd &k, hipStream_t waiter, hipStream_t on) {
+    const hipEvent_t e = mark(k, on);
+    return e && hipStreamWaitEvent(waiter, e, 0) == hipSuccess ? CISTA_OK : CISTA_ERR_HIP;
+}
+template <class F>
+int on_side(Bwd &k, F &&fn) {
+    if (!k.side) return fn();
+    const int rw = stream_wait(k, k.side, k.st);
+    if (rw != CISTA_OK) return rw;
+    const hipStream_t m = k.st;
+    float *const p = k.ws.part, *const bp = k.ws.bpart;
+    k.st = k.side;
+    k.ws.part = k.ws.part2;
+    k.ws.bpart = k.ws.bpart2;
+    const int r = fn();
+    k.st = m;
+    k.ws.part = p;
+    k.ws.bpart = bp;
+    k.side_busy = true;
+    return r;
+}
+int join_side(Bwd &k) {
+    if (!k.side || !k.side_busy) return CISTA_OK;
+    k.side_busy = false;
+    return stream_wait(k, k.st, k.side);
+}
 
 // per-tensor power-of-two scale {s, 1/s} of an output gradient for its fp16 splits (split-f16
 // dgrad and wgrad), in a rotating slot of the backward workspace: the kernel that produces the
@@ -1351,7 +1418,13 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
                        io.c_prev, (const float *)ws.ghb, g.g_c, ws.Gl, io.c_prev ? g.g_c_prev : nullptr, hw, C, scale_slots(k));
     const float *gsc = scale_of(k);
     CHECK_PTR(gsc);
-    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0, pg.lstm_b, gsc));
+    CHECK(on_side(k, [&] {
+        return wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.y, C, io.h_prev, C, 2 * C, h, w, h, w, pg.lstm_w, 1.0f, 0,
+                            pg.lstm_b, gsc);
+    }));
+    // Gl is overwritten by lstc_bwd_kernel (section 6) once this wgrad has read it
+    const hipEvent_t lstm_wgrad_done = k.side ? mark(k, k.side) : nullptr;
+    if (k.side && !lstm_wgrad_done) return CISTA_ERR_HIP;
     if (fold_half) {                                // relu(Dg) mask; h_prev's part if wanted
         CHECK(dgrad_fold(k, CV_LSTM, ws.Gl, gsc, fseg(ws.gy, C, 0, 1.0f, FOLD_MASK, const_cast<float *>(sv.y), scale_slots(k)),
                          fseg(io.h_prev ? g.g_h_prev : nullptr, C, 0), C));
@@ -1363,7 +1436,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
     gsc = scale_of(k);
     CHECK_PTR(gsc);
-    CHECK(wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc));
+    CHECK(on_side(k, [&] {
+        return wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc);
+    }));
     if (fold_half) {                                // g_z + fold
         CHECK(dgrad_fold(k, CV_DG, ws.gy, gsc, fseg(ws.gz, 2 * C, 0, 1.0f, g.g_z ? FOLD_ADD : FOLD_SET, const_cast<float *>(g.g_z)),
                          fseg(nullptr, 0, 0), 2 * C));
@@ -1422,21 +1497,28 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         float *sP = sclD + 2 * D, *sD = sP + 2;
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclP, D, sP);
         hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclD, D, sD);
-        CHECK(wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0, pg.P_b, sP,
-                           D * B));
-        CHECK(wgrad<XS_S1>(k, ws.gxk, C, 0, C, sv.zl, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b, sD,
-                           D * B));
+        CHECK(on_side(k, [&] {
+            const int r = wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0,
+                                       pg.P_b, sP, D * B);
+            if (r != CISTA_OK) return r;
+            return wgrad<XS_S1>(k, ws.gxk, C, 0, C, sv.zl, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.D_w, -1.0f, 0, pg.D_b,
+                                sD, D * B);
+        }));
     }
     // ---- 6. ConvLSTC --------------------------------------------------------------------------
-    // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part)
+    // Gg in Gl (4C: [gi | gf]), Go, gz0 (cell part): Gl held the ConvLSTM gradient that its
+    // side-stream wgrad reads (the ISTA wgrads behind it on that stream keep running)
+    if (lstm_wgrad_done && hipStreamWaitEvent(st, lstm_wgrad_done, 0) != hipSuccess) return CISTA_ERR_HIP;
     hipLaunchKernelGGL(lstc_bwd_kernel, g1d(hw * 2 * C), dim3(256), 0, st, (const float *)sv.gi,
                        (const float *)sv.gf, (const float *)sv.go, (const float *)sv.z0,
                        (const float *)io.c_lstc, io.c_lstc_prev, (const float *)ws.gz, g.g_c_lstc,
                        ws.Gl, ws.Go, ws.gz0, io.c_lstc_prev ? g.g_c_lstc_prev : nullptr, hw, 2 * C, scale_slots(k, 0), scale_slots(k, 1));
     gsc = scale_of(k);                                   // Go; Gl's scale is the next slot set
     CHECK_PTR(gsc);
-    CHECK(wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
-                       pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc));
+    CHECK(on_side(k, [&] {
+        return wgrad<XS_S1>(k, ws.Go, 2 * C, 0, 2 * C, sv.z0, 2 * C, io.z_prev, 2 * C, 4 * C, h, w, h, w,
+                            pg.out_gates_w, 1.0f, 0, pg.out_gates_b, gsc);
+    }));
     const bool want_zp = io.z_prev && g.g_z_prev;
     if (fold_half) {                                // gz0 is final here: its slot set follows Gl's
         CHECK(dgrad_fold(k, CV_OUTG, ws.Go, gsc, fseg(ws.gz0, 2 * C, 0, 1.0f, FOLD_ADD, ws.gz0, scale_slots(k, 1)),
@@ -1449,8 +1531,10 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     gsc = scale_of(k);                                   // Gl (published by lstc_bwd_kernel)
     CHECK_PTR(gsc);
-    CHECK(wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
-                       pg.gates_w, 1.0f, 0, pg.gates_b, gsc));
+    CHECK(on_side(k, [&] {
+        return wgrad<XS_S1>(k, ws.Gl, 4 * C, 0, 4 * C, sv.x1, C, io.z_prev, 2 * C, 3 * C, h, w, h, w,
+                            pg.gates_w, 1.0f, 0, pg.gates_b, gsc);
+    }));
     if (fold_half) {
         CHECK(dgrad_fold(k, CV_GATES, ws.Gl, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1),
                          fseg(want_zp ? g.g_z_prev : nullptr, 2 * C, 0, 1.0f, FOLD_ADD, want_zp ? g.g_z_prev : nullptr), C));
@@ -1461,7 +1545,9 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     }
     gsc = scale_of(k);                                   // gz0 (published by its last fold)
     CHECK_PTR(gsc);
-    CHECK(wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc));
+    CHECK(on_side(k, [&] {
+        return wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc);
+    }));
     if (fold_half) {
         CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
     } else {
@@ -1997,6 +2083,9 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
     if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
         return CISTA_ERR_HIP;
-    return run_backward(k, *params, *io, sv, g, *pg);
+    if (side_enabled() && hipGetDevice(&k.dev) == hipSuccess) k.side = side_stream(k.dev);
+    const int r = run_backward(k, *params, *io, sv, g, *pg);
+    const int j = join_side(k);               // also after a failed call: nothing left running
+    return r != CISTA_OK ? r : j;
 }
 }  // extern "C"
