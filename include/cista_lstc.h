@@ -232,7 +232,10 @@ typedef struct {
 } cista_param_grads;
 
 /* grads_bytes = sizeof(cista_grad_io) as the caller compiled it: members beyond it (fields
- * appended by later ABI versions) are treated as NULL, never read. */
+ * appended by later ABI versions) are treated as NULL, never read.  All results are ordered on
+ * `stream`; the weight gradients run on a library-owned per-device stream forked from and joined
+ * back into `stream` within the call (CISTA_BWD_SIDE=0 in the environment: all on `stream`,
+ * bit-identical results). */
 int cista_backward(const cista_config *cfg, const void *packed, const cista_params *params,
                    int B, int H, int W, const cista_frame_io *io, const void *saved,
                    size_t saved_bytes, const cista_grad_io *grads, size_t grads_bytes,
