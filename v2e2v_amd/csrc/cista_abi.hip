@@ -2083,7 +2083,11 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
     if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
         return CISTA_ERR_HIP;
-    if (side_enabled() && hipGetDevice(&k.dev) == hipSuccess) k.side = side_stream(k.dev);
+    // the side stream is the current device's: used only when the caller's stream is on it
+    hipDevice_t sdev = -1;
+    if (side_enabled() && hipGetDevice(&k.dev) == hipSuccess && hipStreamGetDevice(k.st, &sdev) == hipSuccess &&
+        sdev == k.dev)
+        k.side = side_stream(k.dev);
     const int r = run_backward(k, *params, *io, sv, g, *pg);
     const int j = join_side(k);               // also after a failed call: nothing left running
     return r != CISTA_OK ? r : j;
