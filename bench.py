@@ -186,7 +186,7 @@ def v2e2v_main(args, torch, vd, rank, world, device):
         torch.cuda.synchronize()
         raw_ms = (time.perf_counter() - t_raw) * 1e3 / reps
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:       # the CPU leg: rank 0 at N=1 only
         cpu = v2e2v_cpu_baseline(torch, net, vid, cfgs, B, H, W, P, dt)
     if rank == 0:
         print(json.dumps({
@@ -321,7 +321,7 @@ def train_main(args, torch, vd, rank, world, device):
     roofline["step_frac_est"] = round(train_tf / peak, 4)
     roofline["step_note"] = "whole BPTT step: 3 x forward algorithmic FLOPs per frame x frames/s per GPU"
     cpu = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:       # the CPU leg: rank 0 at N=1 only
         cpu = train_cpu_baseline(torch, model, vox, target, L, H, W)
     if rank == 0:
         print(json.dumps({
@@ -962,19 +962,19 @@ def main():
     layers = time_layers(torch, model, _lib, vox, B, H, W, device, args.layer_reps)
     roofline = dominant_roofline(layers, _lib)
 
-    voxelizer = (time_voxelizer(torch, B * L, args.num_events, nb, H, W, device, cpu_leg=not args.no_cpu_baseline)
-                 if rank == 0 else None)
+    voxelizer = (time_voxelizer(torch, B * L, args.num_events, nb, H, W, device,
+                                cpu_leg=world == 1 and not args.no_cpu_baseline) if rank == 0 else None)
 
     cpu = None
     psnr_vs_ref = rel_vs_ref = erel_vs_ref = parity_sample = None
-    if rank == 0 and not args.no_cpu_baseline:
+    if world == 1 and not args.no_cpu_baseline:       # the CPU leg: rank 0 at N=1 only
         cpu, psnr_vs_ref, rel_vs_ref, erel_vs_ref, parity_sample = cpu_baseline(
             torch, model, vox, H, W, min(args.cpu_frames, L), timed=timed_recs)
 
     if rank == 0:
         frame_ms = sum(v["ms"] * v["launches_per_frame"] for v in layers.values())
         sweep = None
-        if args.sweep:
+        if args.sweep and world == 1:         # single-GPU side measurement
             sweep = batch_sweep(torch, model, args, device, [int(x) for x in args.sweep.split(",") if x])
         cfg_name = f"{H}x{W} {nb}-bin depth={depth} C={C}"
         out = {
