@@ -873,6 +873,7 @@ Saved carve_saved(void *buf, const cista_config &cfg, int B, int H, int W) {
 #endif
 constexpr int WG_BLOCKS = CISTA_WG_BLOCKS;   // wgrad partial-sum blocks per launch (splits x cout/cin blocks)
 constexpr int SCL_PAIRS = 16;                // scale pairs of the non-ISTA gradients of a call (8 used)
+constexpr size_t AMAX_WORDS = (size_t)8 * AMAX_SLOTS * AMAX_STRIDE + 8 * 16;   // slot sets + tickets
 
 struct BwdWs {
     float *gpre, *gU, *dxpF, *ghb, *Gl, *dxp, *gy, *gz, *gv, *gxk, *gx1, *Go, *gz0;
@@ -880,7 +881,8 @@ struct BwdWs {
     float *part, *bpart, *dlp;
     float *part2, *bpart2;   // the side stream's wgrad partials (run_backward, on_side)
     float *wT;          // [9][Cout][Cin] transposed weights for dgrad_vec_kernel
-    unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses)
+    unsigned *amax;     // [8][AMAX_SLOTS * AMAX_STRIDE] gradient |max| slots (zero between uses),
+                        // then [8][16] tickets of ticket_scale (zero between uses)
     float *scl;         // [16] scale pairs
     size_t bytes;
 };
@@ -918,28 +920,17 @@ BwdWs carve_bwd(void *buf, const cista_config &cfg, int B, int H, int W) {
     }
     s.part = take((size_t)WG_BLOCKS * 32 * 32 * 9);
     s.bpart = take((size_t)WG_BLOCKS * 4 * C);
-    s.dlp = take((size_t)2 * C * 512);
+    s.dlp = take((size_t)2 * C * 512 * nd);           // lambda partials [iteration][block][2C]
     s.part2 = take((size_t)WG_BLOCKS * 32 * 32 * 9);
     s.bpart2 = take((size_t)WG_BLOCKS * 4 * C);
     s.wT = take((size_t)9 * C * C);
-    s.amax = reinterpret_cast<unsigned *>(take((size_t)8 * AMAX_SLOTS * AMAX_STRIDE));
+    s.amax = reinterpret_cast<unsigned *>(take(AMAX_WORDS));
     s.scl = take(2 * SCL_PAIRS + 4 * nd + 4);   // the call's pairs, the ISTA P / D pairs per iteration, their minima
     s.bytes = off;
     return s;
 }
 
 inline dim3 g1d(long n) { return dim3((unsigned)((n + 255) / 256)); }
-
-// per-tensor power-of-two scale for an fp16-split dgrad input: {s, 1/s} -> scl
-__device__ __forceinline__ void scale_from_max(float mx, float *scl) {
-    int e = 0;
-    if (mx > 0.0f && isfinite(mx)) {
-        e = (int)floorf(log2f(16384.0f / mx));
-        e = e < -60 ? -60 : (e > 60 ? 60 : e);
-    }
-    scl[0] = ldexpf(1.0f, e);
-    scl[1] = ldexpf(1.0f, -e);
-}
 
 // {s, 1/s} from the |max| slots a producing kernel filled (amax_publish), slots re-zeroed
 __global__ __launch_bounds__(256) void slots_scale_kernel(unsigned *slots, float *scl) {
@@ -1070,6 +1061,17 @@ const float *scale_of(Bwd &k, float *dst) {
     hipLaunchKernelGGL(slots_scale_kernel, dim3(1), dim3(AMAX_SLOTS), 0, k.st, sl, sc);
     return hipGetLastError() == hipSuccess ? sc : nullptr;
 }
+
+// The pair a producer's last block fills (ticket_scale) in place of scale_of's launch: the same
+// pair bookkeeping; the producer publishes into scale_slots(k) and gets ticket_of(k), and the
+// caller calls slot_done(k) after its launch (scale_of's ++slot)
+float *claim_scale(Bwd &k, float *dst = nullptr) {
+    if (dst) return dst;
+    if (k.pair >= SCL_PAIRS) return nullptr;
+    return k.ws.scl + 2 * k.pair++;
+}
+unsigned *ticket_of(Bwd &k) { return k.ws.amax + (size_t)8 * AMAX_SLOTS * AMAX_STRIDE + (size_t)(k.slot & 7) * 16; }
+void slot_done(Bwd &k) { ++k.slot; }
 
 // dst (+)= sign * the split sum of the wgrad partials, and db from the bias partials, one launch
 void reduce_parts_at(Bwd &k, const float *part, const float *bpart, int ns, long n, float *dst, float *db, long nbias,
@@ -1316,7 +1318,8 @@ FoldSeg fseg(float *dst, int Cd, int dc0, float scale = 1.0f, int mode = FOLD_SE
 // input gradient of conv `id` from G (B, Hin, Win, K) with the reflect fold in the conv epilogue:
 // packed columns [0, split) -> s0, [split, N) -> s1 (FoldSeg), then fold_fix_kernel for the
 // reflected border terms.  sc: grad_scale of G.
-int dgrad_fold(Bwd &k, int id, const float *G, const float *sc, const FoldSeg &s0, const FoldSeg &s1, int split) {
+int dgrad_fold(Bwd &k, int id, const float *G, const float *sc, const FoldSeg &s0, const FoldSeg &s1, int split,
+               float *scl_out = nullptr) {
     const ConvShape s = conv_shape(id, k.C);
     const int Hin = id == CV_UP ? k.H : k.h, Win = id == CV_UP ? k.W : k.w;
     // a wave's NW x 16 columns must lie in one FoldSeg: every STAGE_ZP2 configuration of
@@ -1337,6 +1340,11 @@ int dgrad_fold(Bwd &k, int id, const float *G, const float *sc, const FoldSeg &s
     FoldFixArgs f;
     f.fb = k.ws.fb; f.N = s.cin; f.B = k.B; f.n = Hin; f.m = Win;
     f.seg[0] = s0; f.seg[1] = s1; f.fsplit = split;
+    // scl_out: fold_fix's last block turns s0's |max| slots (the interior published by the conv
+    // epilogue, the border by fold_fix) into the pair (ticket_scale)
+    if (scl_out && (!s0.amax || s1.amax)) return CISTA_ERR_INVALID;
+    f.scl = scl_out;
+    f.ticket = scl_out ? ticket_of(k) : nullptr;
     hipLaunchKernelGGL(fold_fix_kernel, g1d((long)k.B * (2 * Win + 2 * (Hin - 2)) * (s.cin / 4)), dim3(256), 0, k.st, f);
     return hip_ok();
 }
@@ -1426,16 +1434,20 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     const hipEvent_t lstm_wgrad_done = k.side ? mark(k, k.side) : nullptr;
     if (k.side && !lstm_wgrad_done) return CISTA_ERR_HIP;
     if (fold_half) {                                // relu(Dg) mask; h_prev's part if wanted
+        float *sgy = claim_scale(k);                // gy's pair, from fold_fix's last block
+        CHECK_PTR(sgy);
         CHECK(dgrad_fold(k, CV_LSTM, ws.Gl, gsc, fseg(ws.gy, C, 0, 1.0f, FOLD_MASK, const_cast<float *>(sv.y), scale_slots(k)),
-                         fseg(io.h_prev ? g.g_h_prev : nullptr, C, 0), C));
+                         fseg(io.h_prev ? g.g_h_prev : nullptr, C, 0), C, sgy));
+        slot_done(k);
+        gsc = sgy;
     } else {
         CHECK(dgrad_conv(k, CV_LSTM, ws.Gl, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gy, C, 0, C, h, w, 1.0f, 0, sv.y, nullptr, nullptr, scale_slots(k)));
         if (io.h_prev && g.g_h_prev) CHECK(fold(k, ws.dxp, 2 * C, C, g.g_h_prev, C, 0, C, h, w, 1.0f, 0, nullptr));
+        gsc = scale_of(k);
+        CHECK_PTR(gsc);
     }
     // ---- 4. Dg conv (+ReLU) ----------------------------------------------------------------
-    gsc = scale_of(k);
-    CHECK_PTR(gsc);
     CHECK(on_side(k, [&] {
         return wgrad<XS_S1>(k, ws.gy, C, 0, C, io.z, 2 * C, nullptr, 0, 2 * C, h, w, h, w, pg.Dg_w, 1.0f, 0, pg.Dg_b, gsc);
     }));
@@ -1462,42 +1474,50 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     for (int it = D - 1; it >= 0; --it) {
         const float *v = sv.v + (size_t)it * hw * 2 * C;
         float *gv = ws.gv + (size_t)it * hw * 2 * C, *gxk = ws.gxk + (size_t)it * hw * C;
-        if (2 * C <= 1024)
+        // dlambda partials per (channel, block) of this iteration in ws.dlp; all iterations'
+        // reduced after the loop (lambda_grad_kernel).  gv's scale pair from the kernel's last block
+        if (2 * C <= 1024) {
             hipLaunchKernelGGL(softshrink_bwd4_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
-        else
+                               lam, gv, ws.dlp + (size_t)it * nbl * 2 * C, hw, 2 * C, scale_slots(k), ticket_of(k),
+                               sclP + 2 * it);
+            slot_done(k);
+            gsc = sclP + 2 * it;
+        } else {
             hipLaunchKernelGGL(softshrink_bwd_kernel, dim3(nbl), dim3(256), 0, st, (const float *)ws.gz, v,
-                               lam, gv, ws.dlp, hw, 2 * C, scale_slots(k));
-        // dlambda partials per (channel, block) in ws.dlp; reduced below (lambda_grad_kernel)
+                               lam, gv, ws.dlp + (size_t)it * nbl * 2 * C, hw, 2 * C, scale_slots(k));
+            gsc = scale_of(k, sclP + 2 * it);
+            CHECK_PTR(gsc);
+        }
         // P: v = z_k + P(x_k) + b_P
-        gsc = scale_of(k, sclP + 2 * it);
-        CHECK_PTR(gsc);
-        if (fold_half) {                            // gx1 += too
-            CHECK(dgrad_fold(k, CV_P, gv, gsc, fseg(gxk, C, 0, 1.0f, FOLD_DST2, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
+        if (fold_half) {                            // gx1 += too; gxk's pair from fold_fix's last block
+            CHECK(dgrad_fold(k, CV_P, gv, gsc, fseg(gxk, C, 0, 1.0f, FOLD_DST2, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C,
+                             sclD + 2 * it));
+            slot_done(k);
+            gsc = sclD + 2 * it;
         } else {
             CHECK(dgrad_conv(k, CV_P, gv, ws.dxp, gsc));
             CHECK(fold(k, ws.dxp, C, 0, gxk, C, 0, C, h, w, 1.0f, 0, nullptr, nullptr, ws.gx1, scale_slots(k)));
+            gsc = scale_of(k, sclD + 2 * it);
+            CHECK_PTR(gsc);
         }
         // D: x_k = x1 - (D(z_k) + b_D)  ->  grad of D's output is -g_xk
-        gsc = scale_of(k, sclD + 2 * it);
-        CHECK_PTR(gsc);
         if (fold_half) {                            // identity path + fold
             CHECK(dgrad_fold(k, CV_D, gxk, gsc, fseg(ws.gz, 2 * C, 0, -1.0f, FOLD_ADD, gv), fseg(nullptr, 0, 0), 2 * C));
         } else {
             CHECK(dgrad_conv(k, CV_D, gxk, ws.dxp, gsc));
             CHECK(fold(k, ws.dxp, 2 * C, 0, ws.gz, 2 * C, 0, 2 * C, h, w, -1.0f, 0, nullptr, gv));
         }
-        // lambda is (1, 2C, 1, 1): sum the per-block partials, accumulate over iterations
-        hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, st, (const float *)ws.dlp, nbl, 2 * C,
-                           pg.lambda, it != D - 1);
     }
     if (D > 0) {
         // tied D / P weights: one wgrad over all iterations each (G and X stacked as D x B samples),
         // the split scale the smallest of the iterations' (their largest gradient)
         float *sP = sclD + 2 * D, *sD = sP + 2;
-        hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclP, D, sP);
-        hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, st, (const float *)sclD, D, sD);
         CHECK(on_side(k, [&] {
+            hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, k.st, (const float *)sclP, D, sP);
+            hipLaunchKernelGGL(min_scale_kernel, dim3(1), dim3(64), 0, k.st, (const float *)sclD, D, sD);
+            // lambda is (1, 2C, 1, 1): the per-block partials of every iteration, summed
+            hipLaunchKernelGGL(lambda_grad_kernel, dim3(2 * C), dim3(256), 0, k.st, (const float *)ws.dlp, nbl, 2 * C, D,
+                               pg.lambda);
             const int r = wgrad<XS_S1>(k, ws.gv, 2 * C, 0, 2 * C, sv.xs, C, nullptr, 0, C, h, w, h, w, pg.P_w, 1.0f, 0,
                                        pg.P_b, sP, D * B);
             if (r != CISTA_OK) return r;
@@ -1548,14 +1568,20 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
     CHECK(on_side(k, [&] {
         return wgrad<XS_S1>(k, ws.gz0, 2 * C, 0, 2 * C, sv.x1, C, nullptr, 0, C, h, w, h, w, pg.P0_w, 1.0f, 0, pg.P0_b, gsc);
     }));
-    if (fold_half) {
-        CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C));
+    const float *gsx = nullptr;                         // gx1 is final: W0's output gradient
+    if (fold_half) {                                    // gx1's pair from fold_fix's last block
+        float *sx = claim_scale(k);
+        CHECK_PTR(sx);
+        CHECK(dgrad_fold(k, CV_P0, ws.gz0, gsc, fseg(ws.gx1, C, 0, 1.0f, FOLD_ADD, ws.gx1, scale_slots(k)), fseg(nullptr, 0, 0), C,
+                         sx));
+        slot_done(k);
+        gsx = sx;
     } else {
         CHECK(dgrad_conv(k, CV_P0, ws.gz0, ws.dxp, gsc));
         CHECK(fold(k, ws.dxp, C, 0, ws.gx1, C, 0, C, h, w, 1.0f, 1, nullptr, nullptr, nullptr, scale_slots(k)));
+        gsx = scale_of(k);
+        CHECK_PTR(gsx);
     }
-    const float *gsx = scale_of(k);                     // gx1 is final: W0's output gradient
-    CHECK_PTR(gsx);
     // ---- 7. W0 (stride 2) over x_full = cat(We(events), Wi(prev_image)), recomputed ----------
     float *xfull = ws.gU, *gxfull = ws.gU;   // x_full is dead once W0's wgrad has run
     {
@@ -2081,7 +2107,7 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     k.pair = 0;
     if (workspace_bytes < k.ws.bytes) return CISTA_ERR_WORKSPACE;
     // the gradient |max| slots start at zero (slots_scale_kernel re-zeroes the ones it reads)
-    if (hipMemsetAsync(k.ws.amax, 0, (size_t)8 * AMAX_SLOTS * AMAX_STRIDE * sizeof(unsigned), k.st) != hipSuccess)
+    if (hipMemsetAsync(k.ws.amax, 0, AMAX_WORDS * sizeof(unsigned), k.st) != hipSuccess)
         return CISTA_ERR_HIP;
     // the side stream is the current device's: used only when the caller's stream is on it
     hipDevice_t sdev = -1;

@@ -64,6 +64,62 @@ __device__ __forceinline__ void amax_publish(unsigned *slots, float m) {
         if (b > 0.0f) atomicMax(slots + (blockIdx.x & (AMAX_SLOTS - 1)) * AMAX_STRIDE, __float_as_uint(b));
     }
 }
+// per-tensor power-of-two scale for an fp16-split dgrad / wgrad input: {s, 1/s} -> scl
+__device__ __forceinline__ void scale_from_max(float mx, float *scl) {
+    int e = 0;
+    if (mx > 0.0f && isfinite(mx)) {
+        e = (int)floorf(log2f(16384.0f / mx));
+        e = e < -60 ? -60 : (e > 60 ? 60 : e);
+    }
+    scl[0] = ldexpf(1.0f, e);
+    scl[1] = ldexpf(1.0f, -e);
+}
+// The last block of a publishing kernel turns the |max| slots into the scale pair, in place of a
+// slots_scale_kernel launch of its own.  The only data that crosses blocks are the slots' atomics,
+// which execute at the memory side, so no fence is needed (a release fence here writes back the
+// XCD's L2 in every block): each block's thread 0 publishes its maximum with a returning atomic
+// and consumes the result (the wave waits until the memory side has performed it), then takes a
+// ticket with a relaxed device-scope atomic; the block that takes the last ticket reads and
+// re-zeroes the slots with atomic exchanges, writes {s, 1/s} (read by the next launch) and re-arms
+// the ticket.  A maximum does not depend on the order of the blocks, so the pair is the one the
+// separate launch computes.  Every block of the grid must call it (no early exits).
+__device__ __forceinline__ void ticket_scale(const float *red4, unsigned *slots, unsigned *ticket, float *scl) {
+    __shared__ int last;
+    __shared__ float red[4];
+    if (threadIdx.x == 0) {
+        const float b = fmaxf(fmaxf(red4[0], red4[1]), fmaxf(red4[2], red4[3]));
+        unsigned old = 0u;
+        if (b > 0.0f)
+            old = __hip_atomic_fetch_max(slots + (blockIdx.x & (AMAX_SLOTS - 1)) * AMAX_STRIDE, __float_as_uint(b),
+                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("" ::"v"(old) : "memory");   // performed before the ticket below
+        last = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1 ? 1 : 0;
+    }
+    __syncthreads();
+    if (!last) return;
+    float m = 0.0f;
+    for (int i = threadIdx.x; i < AMAX_SLOTS; i += blockDim.x)
+        m = fmaxf(m, __uint_as_float(__hip_atomic_exchange(slots + i * AMAX_STRIDE, 0u, __ATOMIC_RELAXED,
+                                                           __HIP_MEMORY_SCOPE_AGENT)));
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = m;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        float b = red[0];
+        for (int w = 1; w < (int)(blockDim.x >> 6); ++w) b = fmaxf(b, red[w]);
+        scale_from_max(b, scl);
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+// amax_publish's block reduction without the atomic (ticket_scale publishes it): red4 <- the
+// block's four wave maxima
+__device__ __forceinline__ void amax_block(float *red4, float m) {
+    __syncthreads();                            // a previous call's reads of red4 are done
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if ((threadIdx.x & 63) == 0) red4[threadIdx.x >> 6] = m;
+    __syncthreads();
+}
+
 __global__ __launch_bounds__(256) void fold_reflect_kernel(const FoldArgs a) {
     const int g4 = a.n / 4;
     const long total = (long)a.B * a.H * a.W * g4;
@@ -119,6 +175,8 @@ struct FoldFixArgs {
     int N, B, n, m;
     FoldSeg seg[2];
     int fsplit;
+    float *scl;             // non-NULL: the last block turns seg[0].amax into this pair (ticket_scale)
+    unsigned *ticket;
 };
 
 __global__ __launch_bounds__(256) void fold_fix_kernel(const FoldFixArgs a) {
@@ -174,6 +232,12 @@ __global__ __launch_bounds__(256) void fold_fix_kernel(const FoldFixArgs a) {
             w.x += f.x; w.y += f.y; w.z += f.z; w.w += f.w;
             *d2 = w;
         }
+    }
+    if (a.scl) {                          // the host passes a pair only with seg[0].amax alone
+        __shared__ float red4[4];
+        amax_block(red4, s1 ? 0.0f : mx);
+        ticket_scale(red4, a.seg[0].amax, a.ticket, a.scl);
+        return;
     }
     if (a.seg[0].amax) amax_publish(a.seg[0].amax, s1 ? 0.0f : mx);
     if (a.seg[1].amax) amax_publish(a.seg[1].amax, s1 ? mx : 0.0f);
@@ -1910,7 +1974,8 @@ __global__ __launch_bounds__(256) void softshrink_bwd_kernel(const float *gz, co
 __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, const float *v,
                                                               const float *lam, float *gv,
                                                               float *dl_partial, long npix, int C,
-                                                              unsigned *amax) {
+                                                              unsigned *amax, unsigned *ticket = nullptr,
+                                                              float *scl = nullptr) {
     __shared__ float4 red[256];
     float mx = 0.0f;
     const int cq = C >> 2, c = (threadIdx.x % cq) * 4, nl = (256 / cq) * cq;
@@ -1943,24 +2008,38 @@ __global__ __launch_bounds__(256) void softshrink_bwd4_kernel(const float *gz, c
         }
         *reinterpret_cast<float4 *>(dl_partial + (size_t)blockIdx.x * C + 4 * threadIdx.x) = s;
     }
-    if (amax) amax_publish(amax, mx);
+    if (amax && scl) {
+        __shared__ float red4[4];
+        amax_block(red4, mx);
+        ticket_scale(red4, amax, ticket, scl);
+    } else if (amax) {
+        amax_publish(amax, mx);
+    }
 }
 
 // dlambda[c] (+)= sum over the nbl per-block partials ([block][c]) of softshrink_bwd_kernel;
 // one workgroup per channel, tree reduction
-__global__ __launch_bounds__(256) void lambda_grad_kernel(const float *dlp, int nbl, int C, float *dst,
-                                                          int accumulate) {
+// dst[c] = sum over the ISTA iterations, the last one first (the backward's order), of the
+// per-block partials dlp[it][b][c] -- the fixed-order block sum of each iteration, then the
+// running sum over iterations (one launch for all of them, after the ISTA loop)
+__global__ __launch_bounds__(256) void lambda_grad_kernel(const float *dlp, int nbl, int C, int niter, float *dst) {
     __shared__ float red[256];
     const int c = blockIdx.x;
-    float s = 0.0f;
-    for (int b = threadIdx.x; b < nbl; b += 256) s += dlp[(size_t)b * C + c];
-    red[threadIdx.x] = s;
-    __syncthreads();
-    for (int k = 128; k > 0; k >>= 1) {
-        if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+    float acc = 0.0f;
+    for (int it = niter - 1; it >= 0; --it) {
+        const float *p = dlp + (size_t)it * nbl * C;
+        float s = 0.0f;
+        for (int b = threadIdx.x; b < nbl; b += 256) s += p[(size_t)b * C + c];
+        __syncthreads();                       // the previous iteration's red[0] has been read
+        red[threadIdx.x] = s;
         __syncthreads();
+        for (int k = 128; k > 0; k >>= 1) {
+            if ((int)threadIdx.x < k) red[threadIdx.x] += red[threadIdx.x + k];
+            __syncthreads();
+        }
+        acc = acc + red[0];                    // the first: 0 + s, as a fresh accumulation
     }
-    if (threadIdx.x == 0) dst[c] = (accumulate ? dst[c] : 0.0f) + red[0];
+    if (threadIdx.x == 0) dst[c] = acc;
 }
 
 // ConvLSTC cell backward (reference base_layers.py:52-71), per (pixel, channel), Cz = 2C:
