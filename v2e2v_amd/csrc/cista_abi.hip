@@ -985,13 +985,24 @@ hipStream_t side_stream(int dev) {
         streams[dev] = nullptr;
     return streams[dev];
 }
+// the calling thread's events on device dev, all created on first use (NULL: could not be;
+// cista_backward then keeps everything on the caller's stream)
+hipEvent_t *event_pool(int dev) {
+    thread_local hipEvent_t pool[MAX_DEV][BWD_EVENTS] = {};
+    if (dev < 0 || dev >= MAX_DEV) return nullptr;
+    for (int i = 0; i < BWD_EVENTS; ++i)
+        if (!pool[dev][i] && hipEventCreateWithFlags(&pool[dev][i], hipEventDisableTiming) != hipSuccess) {
+            pool[dev][i] = nullptr;
+            return nullptr;
+        }
+    return pool[dev];
+}
 // an event recorded on `on` now (NULL on failure)
 hipEvent_t mark(Bwd &k, hipStream_t on) {
-    thread_local hipEvent_t pool[MAX_DEV][BWD_EVENTS] = {};
-    if (k.dev < 0 || k.dev >= MAX_DEV || k.nev >= BWD_EVENTS) return nullptr;
-    hipEvent_t &e = pool[k.dev][k.nev++];
-    if (!e && hipEventCreateWithFlags(&e, hipEventDisableTiming) != hipSuccess) e = nullptr;
-    return e && hipEventRecord(e, on) == hipSuccess ? e : nullptr;
+    hipEvent_t *pool = event_pool(k.dev);
+    if (!pool || k.nev >= BWD_EVENTS) return nullptr;
+    const hipEvent_t e = pool[k.nev++];
+    return hipEventRecord(e, on) == hipSuccess ? e : nullptr;
 }
 // `waiter` waits for the work issued to `on` so far
 int stream_wait(Bwd &k, hipStream_t waiter, hipStream_t on) {
@@ -2112,7 +2123,7 @@ int cista_backward(const cista_config *cfg, const void *packed, const cista_para
     // the side stream is the current device's: used only when the caller's stream is on it
     hipDevice_t sdev = -1;
     if (side_enabled() && hipGetDevice(&k.dev) == hipSuccess && hipStreamGetDevice(k.st, &sdev) == hipSuccess &&
-        sdev == k.dev)
+        sdev == k.dev && event_pool(k.dev))
         k.side = side_stream(k.dev);
     const int r = run_backward(k, *params, *io, sv, g, *pg);
     const int j = join_side(k);               // also after a failed call: nothing left running
