@@ -2,7 +2,9 @@
 # Same-box A/B of the stacked ISTA P wgrad launch (scripts/train_wgrad_bench.py) over the libraries
 # in v2e2v_amd/variants/: HIP-event launch time (3 interleaved passes), then the HBM bytes of each
 # arm (FETCH_SIZE / WRITE_SIZE passes of their own), then the training bench (scripts/ab_train.sh).
-# Writes gpurun_out/wt_ab.txt and gpurun_out/wtpmc_<arm>_<counter>/.
+# Writes gpurun_out/wt_ab.txt and gpurun_out/wtpmc_<arm>_<counter>/.  The round-6 arms were built
+# from commit 8ce774e (build_variants.sh wt_blk "-DCISTA_WT_XCD=0" wt_xcd "-DCISTA_WT_XCD=1"); the
+# switch is gone since, so at later commits any two libraries can be compared this way.
 set -o pipefail
 mkdir -p gpurun_out
 cd /tmp && export TMPDIR=/tmp && cd - > /dev/null
