@@ -1399,21 +1399,37 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
         d.G = ws.gpre; d.Gc = 1; d.Goff = 0; d.W = P.final_w; d.dX = ws.gU; d.Xc = C; d.Xoff = 0;
         d.mask = sv.u; d.B = B; d.Hin = H; d.Win = W; d.Hout = H; d.Wout = W; d.S = 1; d.Cout = 1; d.Cin = C;
         d.accumulate = 0;
-        if (C % 8 == 0) {                                                               // g_U (ReLU'd)
+        const float *gsu = nullptr;
+        if (C % 8 == 0 && C / 8 <= 256) {                                               // g_U (ReLU'd)
+            // pixels in a grid-stride loop (weights in registers), <= 8 workgroups per CU; the
+            // scale pair of gU from the kernel's last block
+            float *sc = claim_scale(k);
+            CHECK_PTR(sc);
+            const long ppb = 256 / (C / 8), nblk = (HW + ppb - 1) / ppb;
+            const dim3 grid((unsigned)(nblk < 8 * NCU ? nblk : 8 * NCU));
             hipLaunchKernelGGL(transpose_w_kernel, g1d((long)C * 9), dim3(256), 0, st, P.final_w, 1, C, ws.wT);
-            hipLaunchKernelGGL(dgrad_final_kernel, g1d(HW * (C / 8)), dim3(256), 0, st, (const float *)ws.gpre,
-                               (const float *)ws.wT, (const float *)sv.u, ws.gU, B, H, W, C, scale_slots(k));
+            if (HW + (long)grid.x * ppb < INT32_MAX)
+                hipLaunchKernelGGL(dgrad_final_kernel<int>, grid, dim3(256), 0, st, (const float *)ws.gpre, (const float *)ws.wT,
+                                   (const float *)sv.u, ws.gU, B, H, W, C, scale_slots(k), ticket_of(k), sc);
+            else
+                hipLaunchKernelGGL(dgrad_final_kernel<long>, grid, dim3(256), 0, st, (const float *)ws.gpre, (const float *)ws.wT,
+                                   (const float *)sv.u, ws.gU, B, H, W, C, scale_slots(k), ticket_of(k), sc);
             CHECK(hip_ok());
+            slot_done(k);
+            gsu = sc;
         } else {
             CHECK(dgrad_vec(k, d, P.final_w));
             hipLaunchKernelGGL(absmax_publish_kernel, dim3(1024), dim3(256), 0, st, (const float *)ws.gU, (long)HW * C,
                                scale_slots(k));
+            gsu = scale_of(k);
+            CHECK_PTR(gsu);
         }
         // upsample conv wgrad as a stride-1 wgrad over the materialised up(h) (in dxpF, which
         // the dgrad below overwrites); the gradient scale is shared with that dgrad
-        const float *gsu = scale_of(k);
-        CHECK_PTR(gsu);
-        hipLaunchKernelGGL(upsample2x_kernel, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
+        if (HW * (C / 4) < INT32_MAX)
+            hipLaunchKernelGGL(upsample2x_kernel<int>, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
+        else
+            hipLaunchKernelGGL(upsample2x_kernel<long>, g1d(HW * (C / 4)), dim3(256), 0, st, io.h, ws.dxpF, B, h, w, C);
         CHECK(wgrad<XS_S1>(k, ws.gU, C, 0, C, ws.dxpF, C, nullptr, 0, C, H, W, H, W, pg.up_w, 1.0f, 0, pg.up_b, gsu));
         float *gup = ws.gU;                              // g wrt up(h)
         if (fold_full) {
@@ -1423,8 +1439,12 @@ int run_backward(Bwd &k, const cista_params &P, const cista_frame_io &io, const 
             CHECK(dgrad_conv(k, CV_UP, ws.gU, ws.dxpF, gsu));
             CHECK(fold(k, ws.dxpF, C, 0, ws.gU, C, 0, C, H, W, 1.0f, 0, nullptr));
         }
-        hipLaunchKernelGGL(upsample_bwd_kernel, g1d(hw * C / 4), dim3(256), 0, st, (const float *)gup, ws.ghb,
-                           B, h, w, C, 1);
+        if (hw * C / 4 < INT32_MAX)
+            hipLaunchKernelGGL(upsample_bwd_kernel<int>, g1d(hw * C / 4), dim3(256), 0, st, (const float *)gup, ws.ghb,
+                               B, h, w, C, 1);
+        else
+            hipLaunchKernelGGL(upsample_bwd_kernel<long>, g1d(hw * C / 4), dim3(256), 0, st, (const float *)gup, ws.ghb,
+                               B, h, w, C, 1);
     } else {
         if (hipMemsetAsync(pg.final_b, 0, 4, st) != hipSuccess ||
             hipMemsetAsync(pg.final_w, 0, (size_t)9 * C * 4, st) != hipSuccess ||

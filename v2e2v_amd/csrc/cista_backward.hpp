@@ -1539,14 +1539,16 @@ __global__ __launch_bounds__(256) void wgrad_in_kernel(const WgradInArgs a) {
 // up = interpolate(x, 2x, bilinear, align_corners=False) materialised, NHWC (B,h,w,C) ->
 // (B,2h,2w,C), the operation order of the forward's STAGE_UP gather (base_layers.py:198), so
 // the upsample conv's wgrad can run as a stride-1 wgrad on it
+template <typename I>     // the element index type (int when the count fits 31 bits)
 __global__ __launch_bounds__(256) void upsample2x_kernel(const float *x, float *up, int B, int h, int w, int C) {
     const int c4 = C / 4, H = 2 * h, W = 2 * w;
-    const long total = (long)B * H * W * c4;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const I total = (I)B * H * W * c4;
+    const I idx = (I)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
     const int q = (int)(idx % c4);
-    const long pix = idx / c4;
-    const int X = (int)(pix % W), Y = (int)((pix / W) % H), b = (int)(pix / ((long)W * H));
+    const I pix = idx / c4;
+    const I row = pix / W;
+    const int X = (int)(pix - row * W), Y = (int)(row % H), b = (int)(row / H);
     const float sy = fmaxf(((float)Y + 0.5f) * 0.5f - 0.5f, 0.0f);
     const float sx = fmaxf(((float)X + 0.5f) * 0.5f - 0.5f, 0.0f);
     const int y0 = (int)sy, x0 = (int)sx;
@@ -1778,43 +1780,72 @@ __global__ __launch_bounds__(256) void dgrad_vec_kernel(const DgradSmallArgs a, 
 // = [u > 0] * sum over (P, t) with reflect(P + t - 1) == Q of G[P] W[t][c].  Thread = (pixel, 8
 // channels): two float4 weight loads ([9][C] layout, L1-resident) per tap feed 8 FMAs; the
 // general dgrad_vec_kernel spent 4 threads and 64-bit index math per such group (211 us at B=8).
+// Pixels in a grid-stride loop, a thread = 8 channels of one pixel per step, so that the 9 x 8
+// weights of the thread's channels are loaded once, into registers.  Interior pixels (2 <= y <=
+// H-3, 2 <= x <= W-3) take refl_taps' three taps per axis in its order -- (y-1, tap 2), (y, 1),
+// (y+1, 0) -- with those registers; the border pixels walk refl_taps and read the weights from
+// memory.  Same products in the same order either way.  I: the pixel index type (int when B x H
+// x W fits 31 bits, chosen by the host; memory offsets are size_t).
+template <typename I>
 __global__ __launch_bounds__(256) void dgrad_final_kernel(const float *G, const float *WT, const float *mask,
                                                           float *dX, int B, int H, int W, int C,
-                                                          unsigned *amax) {
-    const int c8 = C >> 3;
-    const long total = (long)B * H * W * c8;
-    const long idx0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
-    const bool live = idx0 < total;
-    if (!amax && !live) return;
-    const long idx = live ? idx0 : total - 1;
-    const int c = (int)(idx % c8) * 8;
-    const long pix = idx / c8;
-    const int plane = H * W;
-    const int b = (int)(pix / plane), r = (int)(pix - (long)b * plane);
-    const int y = r / W, x = r - y * W;
-    int Py[6], Ty[6], Px[6], Tx[6];
-    const int ny = refl_taps(y, H, H, 1, Py, Ty), nx = refl_taps(x, W, W, 1, Px, Tx);
-    const float *g = G + (size_t)b * plane;
-    float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
-    for (int i = 0; i < ny; ++i)
-        for (int j = 0; j < nx; ++j) {
-            const float gv = g[Py[i] * W + Px[j]];
-            const float *w = WT + (Ty[i] * 3 + Tx[j]) * C + c;
-            const float4 w0 = *reinterpret_cast<const float4 *>(w), w1 = *reinterpret_cast<const float4 *>(w + 4);
+                                                          unsigned *amax, unsigned *ticket = nullptr,
+                                                          float *scl = nullptr) {
+    const int c8 = C >> 3, ppb = 256 / c8;                     // threads per pixel, pixels per block-step
+    const bool lane_on = (int)threadIdx.x < ppb * c8;
+    const int c = ((int)threadIdx.x % c8) * 8;
+    float4 wr0[9], wr1[9];
+#pragma unroll
+    for (int t = 0; t < 9; ++t) {
+        wr0[t] = *reinterpret_cast<const float4 *>(WT + t * C + c);
+        wr1[t] = *reinterpret_cast<const float4 *>(WT + t * C + c + 4);
+    }
+    const I plane = (I)H * W, npix = (I)B * plane;
+    float mx = 0.0f;
+    for (I pix = (I)blockIdx.x * ppb + (I)threadIdx.x / c8; lane_on && pix < npix; pix += (I)gridDim.x * ppb) {
+        const I b = pix / plane, r = pix - b * plane;
+        const int y = (int)(r / W), x = (int)(r - (I)y * W);
+        const float *g = G + (size_t)b * plane;
+        float4 s0 = make_float4(0.f, 0.f, 0.f, 0.f), s1 = s0;
+        auto tap = [&](float gv, const float4 &w0, const float4 &w1) __attribute__((always_inline)) {
             s0.x = fmaf(gv, w0.x, s0.x); s0.y = fmaf(gv, w0.y, s0.y); s0.z = fmaf(gv, w0.z, s0.z); s0.w = fmaf(gv, w0.w, s0.w);
             s1.x = fmaf(gv, w1.x, s1.x); s1.y = fmaf(gv, w1.y, s1.y); s1.z = fmaf(gv, w1.z, s1.z); s1.w = fmaf(gv, w1.w, s1.w);
+        };
+        if (y >= 2 && y <= H - 3 && x >= 2 && x <= W - 3) {
+#pragma unroll
+            for (int i = 0; i < 3; ++i)
+#pragma unroll
+                for (int j = 0; j < 3; ++j) {
+                    const int t = (2 - i) * 3 + (2 - j);
+                    tap(g[(size_t)(y - 1 + i) * W + (x - 1 + j)], wr0[t], wr1[t]);
+                }
+        } else {
+            int Py[6], Ty[6], Px[6], Tx[6];
+            const int ny = refl_taps(y, H, H, 1, Py, Ty), nx = refl_taps(x, W, W, 1, Px, Tx);
+            for (int i = 0; i < ny; ++i)
+                for (int j = 0; j < nx; ++j) {
+                    const float *w = WT + (Ty[i] * 3 + Tx[j]) * C + c;
+                    tap(g[(size_t)Py[i] * W + Px[j]], *reinterpret_cast<const float4 *>(w),
+                        *reinterpret_cast<const float4 *>(w + 4));
+                }
         }
-    const size_t o = (size_t)pix * C + c;
-    const float4 m0 = *reinterpret_cast<const float4 *>(mask + o), m1 = *reinterpret_cast<const float4 *>(mask + o + 4);
-    s0.x = m0.x > 0.0f ? s0.x : 0.0f; s0.y = m0.y > 0.0f ? s0.y : 0.0f;
-    s0.z = m0.z > 0.0f ? s0.z : 0.0f; s0.w = m0.w > 0.0f ? s0.w : 0.0f;
-    s1.x = m1.x > 0.0f ? s1.x : 0.0f; s1.y = m1.y > 0.0f ? s1.y : 0.0f;
-    s1.z = m1.z > 0.0f ? s1.z : 0.0f; s1.w = m1.w > 0.0f ? s1.w : 0.0f;
-    if (live) {
+        const size_t o = (size_t)pix * C + c;
+        const float4 m0 = *reinterpret_cast<const float4 *>(mask + o), m1 = *reinterpret_cast<const float4 *>(mask + o + 4);
+        s0.x = m0.x > 0.0f ? s0.x : 0.0f; s0.y = m0.y > 0.0f ? s0.y : 0.0f;
+        s0.z = m0.z > 0.0f ? s0.z : 0.0f; s0.w = m0.w > 0.0f ? s0.w : 0.0f;
+        s1.x = m1.x > 0.0f ? s1.x : 0.0f; s1.y = m1.y > 0.0f ? s1.y : 0.0f;
+        s1.z = m1.z > 0.0f ? s1.z : 0.0f; s1.w = m1.w > 0.0f ? s1.w : 0.0f;
         *reinterpret_cast<float4 *>(dX + o) = s0;
         *reinterpret_cast<float4 *>(dX + o + 4) = s1;
+        mx = amax4f(amax4f(mx, s0), s1);
     }
-    if (amax) amax_publish(amax, live ? amax4f(amax4f(0.0f, s0), s1) : 0.0f);
+    if (amax && scl) {                        // the scale pair from the last block (ticket_scale)
+        __shared__ float red4[4];
+        amax_block(red4, mx);
+        ticket_scale(red4, amax, ticket, scl);
+    } else if (amax) {
+        amax_publish(amax, mx);
+    }
 }
 
 // W0 (stride 2) dgrad on the zero-padded input domain: dxp (B, H+2, W+2, Cin) gets
@@ -2101,16 +2132,17 @@ __device__ __forceinline__ int up_weights(int y, int n, float (&w)[6], int (&Y)[
 
 // thread = (half-res pixel, 4 channels): the tap weights once per 4 channels, float4 loads; the
 // per-channel sums keep the scalar kernel's order (rows i, then columns j)
+template <typename I>     // the element index type (int when the count fits 31 bits)
 __global__ void upsample_bwd_kernel(const float *gup, float *gh, int B, int h, int w, int C,
                                     int accumulate) {
     const int cq = C >> 2;
-    const long total = (long)B * h * w * cq;
-    const long idx = (long)blockIdx.x * blockDim.x + threadIdx.x;
+    const I total = (I)B * h * w * cq;
+    const I idx = (I)blockIdx.x * blockDim.x + threadIdx.x;
     if (idx >= total) return;
     const int c = (int)(idx % cq) * 4;
-    const long pix = idx / cq;
+    const I pix = idx / cq;
     const int plane = h * w;
-    const int b = (int)(pix / plane), r = (int)(pix - (long)b * plane);
+    const int b = (int)(pix / plane), r = (int)(pix - (I)b * plane);
     const int y = r / w, x = r - y * w;
     float wy[6], wx[6];
     int Ys[6], Xs[6];
