@@ -428,27 +428,30 @@ def test_training_two_region_tiling_equals_single():
         assert e1 < 1e-5 and e2 < 1e-5, (i, e1, e2)
 
 
-def test_side_stream_wgrads_bit_identical(monkeypatch):
+@pytest.mark.parametrize("H,W,C,B", [(180, 240, 64, 8), (6, 8, 32, 2), (10, 14, 128, 2)])
+def test_side_stream_wgrads_bit_identical(monkeypatch, H, W, C, B):
     """The backward's weight gradients run on a side stream beside the dgrad chain
     (cista_abi.hip on_side / join_side).  They are the same kernels on the same inputs, so a BPTT
-    step at config c3's shape (180x240, B=8, 3 frames) gives bit-identical parameter and input
-    gradients with the side stream on and off (CISTA_BWD_SIDE, read per call); a missed
-    write-after-read hazard between the two streams would show up here as a differing value."""
-    B, L = 8, 3
-    m = CistaLSTCNet([180, 240], base_channels=64, depth=5, num_bins=5)
-    params = fx.stress_params(64, 5, 5, seed=43, lam=0.05)
+    step (3 frames) gives bit-identical parameter and input gradients with the side stream on and
+    off (CISTA_BWD_SIDE, read per call); a missed write-after-read hazard between the two streams
+    would show up here as a differing value.  Shapes: config c3's (180x240, B=8; the folded
+    dgrads with their scale tickets), 6x8 at C = 32 (half-res 3x4: the padded-domain dgrad +
+    fold pass and scale_of launches) and 10x14 at C = 128 (other channel counts on both streams)."""
+    L = 3
+    m = CistaLSTCNet([H, W], base_channels=C, depth=5, num_bins=5)
+    params = fx.stress_params(C, 5, 5, seed=43, lam=0.05)
     sd = fx.expand_tied({k: torch.from_numpy(np.ascontiguousarray(v)) for k, v in params.items()}, 5)
     m.load_state_dict(sd, strict=True)
     m = m.to(DEV)
     rng = np.random.default_rng(9)
-    vox = rng.standard_normal((L, B, 5, 180, 240)).astype(np.float32)
-    target = gpu(rng.random((B, 1, 180, 240)).astype(np.float32))
+    vox = rng.standard_normal((L, B, 5, H, W)).astype(np.float32)
+    target = gpu(rng.random((B, 1, H, W)).astype(np.float32))
 
     def step(side):
         monkeypatch.setenv("CISTA_BWD_SIDE", "1" if side else "0")
         m.zero_grad(set_to_none=True)
         evs = [gpu(vox[f], True) for f in range(L)]
-        prev, state = torch.zeros(B, 1, 180, 240, device=DEV), None
+        prev, state = torch.zeros(B, 1, H, W, device=DEV), None
         for f in range(L):
             out, state = m(evs[f], prev, state)
             prev = out.clone()
